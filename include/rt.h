@@ -1,0 +1,172 @@
+/*
+ * rt.h — C ABI of the MI355X path-tracing hot path (libpsrt.so).
+ *
+ * This is the drop-in boundary for the reference's per-pixel loop. The
+ * reference (fengye/PeterShirleyRaytracer) has no FFI: its hot path is the
+ * pixel loop in main() (programs/main.cc:72-88), which calls
+ * ray_color (programs/main.cc:34-49) -> hittable_list::hit
+ * (programs/hittable_list.cc:3-20) -> sphere::hit (programs/sphere.cc:3-40)
+ * -> vec3::random_in_hemisphere (programs/vec3.h:102-109), and quantises each
+ * pixel with write_color (programs/color.h:8-24). Every entry point below
+ * names the reference code it replaces.
+ *
+ * Conventions
+ *   - 0 = success, negative = error (RT_E_*); rt_last_error() returns a
+ *     thread-local message for the last failing call on this thread.
+ *   - Plain pointers and sizes only. "host" buffers are caller-owned host
+ *     memory; "device" buffers are caller-owned HIP device allocations on the
+ *     context's device; "stream" is a hipStream_t passed as void* (NULL = the
+ *     context's own stream).
+ *   - Pixel order is the reference's output order (main.cc:72-75): output row
+ *     r = 0 is the TOP row (reference j = H-1), columns i = 0..W-1 left to
+ *     right. A shard owns rows r = row_offset + k*row_stride, k = 0,1,...
+ *   - Arithmetic is IEEE binary64 in the reference's operation order, no FMA
+ *     contraction: accumulators are bit-identical to the reference's
+ *     pixel_color (main.cc:77-84) for the same RNG stream.
+ */
+#ifndef PSRT_RT_H
+#define PSRT_RT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* ---- error codes ---------------------------------------------------------- */
+#define RT_OK 0
+#define RT_E_INVALID (-1)  /* bad argument (null pointer, size, shard)          */
+#define RT_E_HIP (-2)      /* HIP runtime failure (message names the hipError) */
+#define RT_E_NODEVICE (-3) /* no HIP device visible                            */
+#define RT_E_NOMEM (-4)    /* device allocation failed                          */
+#define RT_E_SCENE (-5)    /* scene not set / non-sphere object / too large     */
+
+/* ---- scene ---------------------------------------------------------------- */
+
+/* One flattened `sphere` (sphere.h:18-19: point3 centre; double radius).
+ * hittable_list order is preserved: index k is objects[k]
+ * (hittable_list.h:40), which decides ties (hittable_list.cc:11-15). */
+typedef struct {
+  double cx, cy, cz, r;
+} rt_sphere;
+
+/* The camera's public members (camera.h:31-35). get_ray(u,v) is
+ * ray(origin, ((lower_left + horizontal*u) + vertical*v) - origin)
+ * (camera.h:25-28). */
+typedef struct {
+  double origin[3];
+  double lower_left[3];
+  double horizontal[3];
+  double vertical[3];
+} rt_camera;
+
+/* ---- render parameters ----------------------------------------------------- */
+
+/* RNG streams. The reference draws from glibc rand() serially
+ * (random.h:4-14), which no parallel device can reproduce; the device path
+ * uses the COUNTER stream: one PCG32 stream per (pixel, sample), fed through
+ * the reference's own random_double() mapping. See DESIGN.md §RNG. */
+#define RT_RNG_COUNTER 0
+
+/* flags */
+#define RT_FLAG_NONE 0
+#define RT_FLAG_NO_ACCUM 1u /* skip writing FP64 accumulators (rgb8 only)    */
+
+typedef struct {
+  int width;      /* image_width  (main.cc:57)                              */
+  int height;     /* image_height (main.cc:58)                              */
+  int spp;        /* sample_per_pixel (main.cc:66)                          */
+  int max_depth;  /* max_depth (main.cc:68); up to max_depth+1 traced rays  */
+  uint64_t seed;  /* counter-RNG seed                                       */
+  int row_offset; /* first owned output row (0 = top)                       */
+  int row_stride; /* owned rows are row_offset + k*row_stride (>= 1)        */
+  unsigned flags; /* RT_FLAG_*                                              */
+} rt_params;
+
+/* Counters of one render (all ranks' shards add up to the frame's). */
+typedef struct {
+  uint64_t samples;      /* camera samples traced                           */
+  uint64_t rays;         /* ray_color() invocations that called world.hit   */
+  uint64_t sphere_tests; /* sphere::hit evaluations implied = rays * n      */
+  double kernel_ms;      /* device time of the trace kernels (HIP events)   */
+  double total_ms;       /* wall time inside the call                       */
+} rt_stats;
+
+/* Number of rows a shard owns. */
+int rt_rows_owned(int height, int row_offset, int row_stride);
+
+/* ---- one-shot API (host buffers) ------------------------------------------ */
+
+/* Replaces main.cc:72-88 for the owned rows: traces spp samples per pixel and
+ * writes the FP64 pixel_color sums (rows_owned x width x 3, reference pixel
+ * order) into accum_rgb (host) and, if rgb8 != NULL, the write_color bytes
+ * (rows_owned x width x 3) into rgb8 (host). stats may be NULL.
+ * Uses device 0 (or RT_DEVICE env). */
+int rt_render(const rt_sphere* spheres, int n_spheres, const rt_camera* cam,
+              const rt_params* params, double* accum_rgb, unsigned char* rgb8,
+              rt_stats* stats);
+
+/* write_color (color.h:8-24) on host data: (int)(255.999*clamp(sqrt(c*(1/spp)),0,0.999)). */
+int rt_quantize_ppm(const double* accum_rgb, int width, int rows, int spp,
+                    unsigned char* rgb8);
+
+/* ---- context API (device-resident buffers, async) ------------------------- */
+
+typedef struct rt_context rt_context;
+
+int rt_context_create(int device, rt_context** out);
+int rt_context_destroy(rt_context* ctx);
+
+/* Flattened hittable_list + camera -> device constant buffers. */
+int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres,
+                         int n_spheres, const rt_camera* cam);
+
+/* Enqueue a render of the owned rows on `stream`. d_accum (device,
+ * rows_owned*width*3 doubles) and d_rgb8 (device, rows_owned*width*3 bytes)
+ * may each be NULL. Returns after enqueueing; synchronise the stream before
+ * reading. rt_context_last_stats() reports the finished call's counters. */
+int rt_render_device(rt_context* ctx, const rt_params* params, double* d_accum,
+                     unsigned char* d_rgb8, void* stream);
+
+/* Wait for the context's last render and fill stats (counters + kernel_ms). */
+int rt_context_sync_stats(rt_context* ctx, rt_stats* stats);
+
+/* Device-side write_color over d_accum (rows*width*3) -> d_rgb8. */
+int rt_quantize_device(rt_context* ctx, const double* d_accum, int width,
+                       int rows, int spp, unsigned char* d_rgb8, void* stream);
+
+/* ---- scene helpers (host) -------------------------------------------------- */
+
+/* camera() default constructor (camera.h:11-23): 16:9, viewport 2 high,
+ * focal length 1, origin 0. */
+int rt_camera_default(rt_camera* out);
+
+/* lookfrom/lookat pinhole (extension; no defocus): the book's
+ * camera(lookfrom, lookat, vup, vfov_degrees, aspect). */
+int rt_camera_look_at(const double lookfrom[3], const double lookat[3],
+                      const double vup[3], double vfov_deg, double aspect,
+                      rt_camera* out);
+
+/* The reference's two-sphere world (main.cc:61-63). Returns the count (2);
+ * writes at most cap records. */
+int rt_scene_two_spheres(rt_sphere* out, int cap);
+
+/* The final random-spheres scene: glibc srand(seed)
+ * stream, ground r=1000, 22x22 jittered r=0.2 grid, three r=1 spheres,
+ * diffuse-only. Returns the sphere count; writes at most cap records. */
+int rt_scene_random_spheres(unsigned int seed, rt_sphere* out, int cap);
+
+/* ---- misc ----------------------------------------------------------------- */
+const char* rt_last_error(void);
+int rt_abi_version(void);
+int rt_device_count(void);
+const char* rt_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PSRT_RT_H */
