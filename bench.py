@@ -1,0 +1,291 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X path-tracing hot path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
+    torchrun --nproc-per-node N bench.py --gpus N ...        (N > 1, RCCL)
+
+A step is one full frame of the configured workload: every rank renders its
+interleaved rows (psrt_trace + psrt_reduce through rt_render_device, inputs
+resident in HBM), the FP64 framebuffer is gathered to rank 0 over RCCL and
+quantised there (write_color, color.h:8-24). Total work is fixed as N grows
+("strong" scaling). Rank 0 prints one JSON line; value = W*H*spp*K / wall,
+wall = max over ranks between barriers.
+
+Default workload (BASELINE.json north star, configs[2]): the final
+random-spheres scene (485 spheres), 1200x800, 100 spp, depth 50.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Msamples/sec (W×H×spp/wall) at 1/2/4/8 GPUs; PSNR vs CPU PPM"
+
+CONFIGS = {
+    "c1": dict(scene="two", width=400, height=225, spp=10,
+               desc="two-sphere world (main.cc:61-63), 400x225, 10 spp, depth 50"),
+    "c2": dict(scene="two", width=1200, height=800, spp=100,
+               desc="two-sphere world (main.cc:61-63), 1200x800, 100 spp, depth 50"),
+    "c3": dict(scene="final", width=1200, height=800, spp=100,
+               desc="final random-spheres scene (485 spheres), 1200x800, 100 spp, depth 50"),
+    "c4": dict(scene="final", width=3840, height=2160, spp=500,
+               desc="final random-spheres scene (485 spheres), 3840x2160, 500 spp, depth 50"),
+    "c5": dict(scene="final", width=1200, height=800, spp=10000,
+               desc="final random-spheres scene (485 spheres), 1200x800, 10000 spp, depth 50"),
+}
+
+# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md): 256 CUs at 2.4 GHz;
+# FP64 vector = half the FP32 vector rate: 16 lanes/clk/SIMD x 4 SIMDs -> one
+# non-FMA FP64 op per lane-slot: 256 * 64 * 2.4e9 = 39.3e12 op/s.
+PEAK_FP64_OPS = 256 * 64 * 2.4e9
+PEAK_HBM = 8.0e12
+# sphere.cc:6-14 per ray-sphere test: amc (3), A (5), HALF_B (5), C (5 + r*r + sub = 7),
+# discriminant (3) = 23 FP64 ops. psrt_trace executes 17 of them per test (A is
+# hoisted per ray, r*r per sphere: the same values) + 1 compare.
+OPS_PER_TEST = 23
+EXEC_OPS_PER_TEST = 18
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--max-depth", type=int, default=50)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="target CPU work of the bounded reference baseline sample")
+    ap.add_argument("--cpu-procs", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--save-ppm", default="")
+    return ap.parse_args()
+
+
+def scene_of(cfg):
+    import petershirleyraytracer_amd as P
+    if cfg["scene"] == "two":
+        return P.scene_two_spheres(), P.camera_default()
+    return P.scene_random_spheres(1), P.camera_look_at(aspect=cfg["width"] / cfg["height"])
+
+
+def cpu_baseline(cfg, args, frame_acc):
+    """The reference itself (oracle/_ref/ref_render: the reference sources
+    compiled unmodified) on a bounded sample of the same workload: a set of
+    rows spread over the frame, columns split over worker processes. Also
+    checks those pixels against the GPU frame bit for bit."""
+    import oracle as O  # checker / baseline only
+    if not O.have_ref():
+        return None, None
+    w, h, spp = cfg["width"], cfg["height"], cfg["spp"]
+    procs = max(1, min(args.cpu_procs, len(os.sched_getaffinity(0))))
+    # per-core reference rate: two-sphere 0.62 Ms/s, final 0.0232 Ms/s
+    rate = 0.62e6 if cfg["scene"] == "two" else 0.0232e6
+    want_samples = args.cpu_seconds * procs * rate
+    rows = max(1, min(h, int(want_samples / (w * spp))))
+    stride = max(1, h // rows)
+    rows = len(range(0, h, stride))
+    spp_eff = spp
+    if rows == 1 and w * spp > want_samples:  # very high spp: shorten the sample count
+        spp_eff = max(1, int(want_samples / w))
+    cols = np.linspace(0, w, procs + 1).astype(int)
+    with tempfile.TemporaryDirectory() as td:
+        cmds = []
+        for p in range(procs):
+            if cols[p + 1] <= cols[p]:
+                continue
+            cmds.append((p, [O.REF_BIN, "--scene", cfg["scene"], "--width", str(w), "--height",
+                             str(h), "--spp", str(spp_eff), "--depth", str(args.max_depth),
+                             "--seed", str(args.seed), "--rows", f"0:{stride}:{rows}",
+                             "--cols", f"{cols[p]}:{cols[p + 1]}",
+                             "--accum", os.path.join(td, f"a{p}.bin")]))
+        t0 = time.perf_counter()
+        running = [(p, subprocess.Popen(c, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE))
+                   for p, c in cmds]
+        ok = all(pr.wait() == 0 for _, pr in running)
+        wall = time.perf_counter() - t0
+        if not ok:
+            return None, None
+        samples = rows * w * spp_eff
+        parity = None
+        if frame_acc is not None and spp_eff == spp:
+            equal, n_pix, sq = True, 0, 0.0
+            for p, _ in cmds:
+                a = np.fromfile(os.path.join(td, f"a{p}.bin"), dtype=np.float64)
+                a = a.reshape(rows, cols[p + 1] - cols[p], 3)
+                g = np.ascontiguousarray(frame_acc[0:h:stride][:rows, cols[p]:cols[p + 1]])
+                equal &= bool(np.array_equal(a.view(np.uint64), g.view(np.uint64)))
+                n_pix += a.shape[0] * a.shape[1]
+                d = O.quantize(a, spp).astype(np.float64) - O.quantize(g, spp)
+                sq += float(np.sum(d * d))
+            mse = sq / max(1, 3 * n_pix)
+            psnr = "inf" if mse == 0 else round(10 * math.log10(255.0 ** 2 / mse), 3)
+            parity = dict(pixels_compared=n_pix, fp64_bit_identical=equal, ppm_psnr_db=psnr)
+    cb = dict(value=samples / wall / 1e6, unit="Msamples/s", cores=procs, kind="reference",
+              sample=(f"{rows} rows (every {stride}th) x {w} cols x {spp_eff} spp "
+                      f"= {samples} samples of the same workload; reference sources "
+                      f"(g++ -O2, unmodified) in {procs} single-thread processes, "
+                      f"{wall:.1f} s wall"))
+    return cb, parity
+
+
+def traffic_from_profile(config: str):
+    """HBM bytes per psrt_trace launch from the committed rocprofv3 PMC
+    summary (profiles/pmc_<config>.json), FETCH_SIZE doubled per the gfx950
+    calibration note in MI355X_MICROARCH.md §HBM."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        return float(d["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    cfg = CONFIGS[args.config]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE",
+              file=sys.stderr)
+
+    import torch
+    import torch.distributed as dist
+
+    import petershirleyraytracer_amd as P
+    from petershirleyraytracer_amd.dist import gather_frame, rows_owned, shard
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    w, h, spp = cfg["width"], cfg["height"], cfg["spp"]
+    spheres, cam = scene_of(cfg)
+    ctx = P.Context(local)
+    ctx.set_scene(spheres, cam)
+    off, stride = shard(rank, world)
+    rows = rows_owned(h, rank, world)
+    prm = P.params(w, h, spp, args.max_depth, args.seed, off, stride)
+    dev = torch.device("cuda", local)
+    acc = torch.zeros((rows, w, 3), dtype=torch.float64, device=dev)
+    rgb = torch.zeros((h, w, 3), dtype=torch.uint8, device=dev) if rank == 0 else None
+    stream = torch.cuda.current_stream(dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    kernel_ms, rays, elapsed = [], [], 0.0
+    frame = None
+    for step in range(args.warmup + args.steps):
+        if step == args.warmup:
+            barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+        if world == 1:
+            ctx.render_device(prm, acc.data_ptr(), rgb.data_ptr(), stream.cuda_stream)
+            frame = acc
+        else:
+            ctx.render_device(prm, acc.data_ptr(), 0, stream.cuda_stream)
+            frame = gather_frame(acc, h, rank, world)
+            if rank == 0:
+                ctx.quantize_device(frame.data_ptr(), w, h, spp, rgb.data_ptr(),
+                                    stream.cuda_stream)
+        st = ctx.sync_stats()
+        if step >= args.warmup:
+            kernel_ms.append(st["kernel_ms"])
+            rays.append(st["rays"])
+    torch.cuda.synchronize(dev)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_samples = w * h * spp * args.steps
+    value = total_samples / elapsed / 1e6
+
+    if rank == 0:
+        n = len(spheres)
+        avg_ms = float(np.mean(kernel_ms))
+        rays_launch = float(np.mean(rays))  # this rank's rays per launch
+        tests = rays_launch * n
+        ops = tests * OPS_PER_TEST
+        achieved = ops / (avg_ms * 1e-3)
+        # algorithmic HBM bytes per launch: per-sample colour written and read
+        # back once (24 B + 24 B) + FP64 accumulators written (24 B per pixel)
+        # + sphere list read per workgroup (L2-resident)
+        samples_rank = rows * w * spp
+        hbm_alg = samples_rank * 24 + rows * w * 24
+        traffic = traffic_from_profile(args.config)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 4),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (procedural scene: final random-spheres, glibc srand(1); counter RNG seed 0)",
+            "config": {"workload": cfg["desc"], "config_id": args.config, "width": w,
+                       "height": h, "spp": spp, "max_depth": args.max_depth, "spheres": n,
+                       "parallelism": f"interleaved rows x{world}" + (", RCCL framebuffer gather" if world > 1 else "")},
+            "roofline": {
+                "bound": "valu",
+                "achieved": round(achieved / 1e12, 4),
+                "peak": round(PEAK_FP64_OPS / 1e12, 2),
+                "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_FP64_OPS, 4),
+                "traffic": traffic,
+                "kernel": "psrt_trace",
+                "avg_launch_ms": round(avg_ms, 3),
+                "rays_per_launch": int(rays_launch),
+                "sphere_tests_per_launch": int(tests),
+                "ops_per_test": OPS_PER_TEST,
+                "executed_ops_per_test": EXEC_OPS_PER_TEST,
+                "note": ("fp64 non-FMA op rate; algorithmic ops = reference sphere tests "
+                         "(rays x spheres) x 23; neither HBM nor MFMA bounds this kernel"),
+                "hbm_algorithmic_bytes_per_launch": hbm_alg,
+                "hbm_frac": round(hbm_alg / (avg_ms * 1e-3) / PEAK_HBM, 6),
+            },
+            "rays_per_sample": round(float(np.sum(rays)) / (rows * w * spp * args.steps), 3),
+        }
+        if args.save_ppm and rgb is not None:
+            P.write_ppm(args.save_ppm, rgb.cpu().numpy(), binary=True)
+        cb, parity = None, None
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                cb, parity = cpu_baseline(cfg, args, frame.cpu().numpy())
+            except Exception as e:  # baseline is reported, never the target
+                print(f"cpu baseline failed: {e}", file=sys.stderr)
+        out["cpu_baseline"] = cb
+        out["parity_vs_cpu"] = parity
+        print(json.dumps(out), flush=True)
+
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -71,9 +71,8 @@ typedef struct {
  * the reference's own random_double() mapping. See DESIGN.md §RNG. */
 #define RT_RNG_COUNTER 0
 
-/* flags */
+/* flags (reserved; must be 0) */
 #define RT_FLAG_NONE 0
-#define RT_FLAG_NO_ACCUM 1u /* skip writing FP64 accumulators (rgb8 only)    */
 
 typedef struct {
   int width;      /* image_width  (main.cc:57)                              */
@@ -127,7 +126,7 @@ int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres,
 /* Enqueue a render of the owned rows on `stream`. d_accum (device,
  * rows_owned*width*3 doubles) and d_rgb8 (device, rows_owned*width*3 bytes)
  * may each be NULL. Returns after enqueueing; synchronise the stream before
- * reading. rt_context_last_stats() reports the finished call's counters. */
+ * reading. rt_context_sync_stats() reports the finished call's counters. */
 int rt_render_device(rt_context* ctx, const rt_params* params, double* d_accum,
                      unsigned char* d_rgb8, void* stream);
 
@@ -164,6 +163,17 @@ const char* rt_last_error(void);
 int rt_abi_version(void);
 int rt_device_count(void);
 const char* rt_build_info(void);
+
+/* Debug: run one binary64 primitive on the device, element-wise
+ * (op 0 sqrt(x), 1 x/y, 2 x*y, 3 x+y, 4 x*y+x uncontracted, 5 ldexp(x,(int)y)).
+ * Used by the numerics parity tests. */
+int rt_debug_probe_f64(int op, const double* x, const double* y, double* out, int n);
+
+/* Debug: hittable_list::hit (hittable_list.cc:3-20) on the device with the
+ * megakernel's own sweep, one ray per thread. rays[k*8..] = {ox,oy,oz,dx,dy,dz,
+ * tmin,tmax}; out[k*9..] = {index (-1 miss), px,py,pz, nx,ny,nz, t, front_face}. */
+int rt_debug_world_hit(const rt_sphere* spheres, int n_spheres, const double* rays,
+                       int count, double* out);
 
 #ifdef __cplusplus
 }

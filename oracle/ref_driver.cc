@@ -51,21 +51,62 @@ struct counting_world : public hittable {
   }
 };
 
+// Known-answer mode: each input line is "n  cx cy cz r (n times)  ox oy oz
+// dx dy dz  tmin tmax" (hex floats); each output line is the reference
+// hittable_list::hit result "index px py pz nx ny nz t front_face" (hex
+// floats; index -1 = miss). The hit sphere's index is recovered by running
+// sphere::hit per object with the final t (the reference records no index).
+int run_kat(const std::string& path) {
+  std::ifstream in(path);
+  std::string line;
+  while (std::getline(in, line)) {
+    if (line.empty()) continue;
+    std::istringstream ss(line);
+    auto rd = [&]() { std::string t; ss >> t; return std::strtod(t.c_str(), nullptr); };
+    int n = (int)rd();
+    hittable_list world;
+    std::vector<std::shared_ptr<sphere>> sp;
+    for (int k = 0; k < n; ++k) {
+      double cx = rd(), cy = rd(), cz = rd(), r = rd();
+      sp.push_back(make_shared<sphere>(point3(cx, cy, cz), r));
+      world.add(sp.back());
+    }
+    double ox = rd(), oy = rd(), oz = rd(), dx = rd(), dy = rd(), dz = rd();
+    double tmin = rd(), tmax = rd();
+    ray r(point3(ox, oy, oz), vec3(dx, dy, dz));
+    hit_record rec;
+    if (!world.hit(r, tmin, tmax, rec)) {
+      std::printf("-1\n");
+      continue;
+    }
+    // which object produced rec: replay the list scan (hittable_list.cc:9-17)
+    int idx = -1;
+    double closest = tmax;
+    hit_record tmp;
+    for (int k = 0; k < n; ++k)
+      if (sp[k]->hit(r, tmin, closest, tmp)) { closest = tmp.t; idx = k; }
+    std::printf("%d %a %a %a %a %a %a %a %d\n", idx, rec.p.x(), rec.p.y(), rec.p.z(),
+                rec.normal.x(), rec.normal.y(), rec.normal.z(), rec.t, (int)rec.front_face);
+  }
+  return 0;
+}
+
 void usage() {
   std::fprintf(stderr,
                "ref_render [--reference-main] [--width W] [--height H] [--spp S]\n"
                "  [--depth D] [--scene two|final] [--scene-seed N] [--rng glibc|counter]\n"
                "  [--seed N] [--rows OFF:STRIDE[:COUNT]] [--accum FILE] [--ppm FILE]\n"
-               "  [--dump-scene FILE] [--camera default|lookat]\n");
+               "  [--dump-scene FILE] [--camera default|lookat] [--kat FILE] [--cols C0:C1]\n");
 }
 
 }  // namespace
 
 int main(int argc, char** argv) {
   int W = 400, H = -1, spp = 10, depth = 50, row_off = 0, row_stride = 1, row_count = -1;
+  int col0 = 0, col1 = -1;  // --cols: render only columns [col0, col1) of each row
   unsigned scene_seed = 1;
   uint64_t seed = 0;
-  std::string scene = "two", rng = "counter", accum_path, ppm_path, dump_path, cam_kind;
+  std::string scene = "two", rng = "counter", accum_path, ppm_path, dump_path, cam_kind, kat_path;
   bool run_reference_main = false;
   for (int a = 1; a < argc; ++a) {
     std::string k = argv[a];
@@ -86,12 +127,18 @@ int main(int argc, char** argv) {
     else if (k == "--ppm") ppm_path = next();
     else if (k == "--dump-scene") dump_path = next();
     else if (k == "--camera") cam_kind = next();
+    else if (k == "--kat") kat_path = next();
+    else if (k == "--cols") {
+      std::string v = next();
+      if (std::sscanf(v.c_str(), "%d:%d", &col0, &col1) != 2) { usage(); return 2; }
+    }
     else if (k == "--rows") {
       std::string v = next();
       if (std::sscanf(v.c_str(), "%d:%d:%d", &row_off, &row_stride, &row_count) < 2) { usage(); return 2; }
     } else { usage(); return 2; }
   }
   if (run_reference_main) return reference_main();
+  if (!kat_path.empty()) return run_kat(kat_path);
 
   // ---- world (main.cc:61-63, or the final scene) ----
   hittable_list world;
@@ -166,13 +213,16 @@ int main(int argc, char** argv) {
   int rows = (H - 1 - row_off) / row_stride + 1;
   if (row_count >= 0 && row_count < rows) rows = row_count;
   counting_world counted(world);
-  std::vector<double> accum((size_t)rows * W * 3);
+  if (col1 < 0 || col1 > W) col1 = W;
+  if (col0 < 0) col0 = 0;
+  const int ncols = col1 > col0 ? col1 - col0 : 0;
+  std::vector<double> accum((size_t)rows * ncols * 3);
   std::ostringstream ppm;
-  ppm << "P3\n" << W << ' ' << rows << "\n255\n";
+  ppm << "P3\n" << ncols << ' ' << rows << "\n255\n";
   auto t0 = std::chrono::steady_clock::now();
   for (int k = 0; k < rows; ++k) {
     int j = H - 1 - (row_off + k * row_stride);
-    for (int i = 0; i < W; ++i) {
+    for (int i = col0; i < col1; ++i) {
       color pixel_color(0, 0, 0);
       for (int s = 0; s < spp; ++s) {
         if (counter) g_counter_state = oracle_stream_state(seed, (uint32_t)(j * W + i), (uint32_t)s);
@@ -180,14 +230,14 @@ int main(int argc, char** argv) {
         double v = ((double)j + random_double()) / (H - 1);
         pixel_color += ray_color(cam.get_ray(u, v), counted, depth);
       }
-      double* px = &accum[((size_t)k * W + i) * 3];
+      double* px = &accum[((size_t)k * ncols + (i - col0)) * 3];
       px[0] = pixel_color.x(), px[1] = pixel_color.y(), px[2] = pixel_color.z();
       write_color(ppm, pixel_color, spp);
     }
   }
   double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   std::fprintf(stderr, "{\"samples\": %llu, \"rays\": %llu, \"seconds\": %.6f}\n",
-               (unsigned long long)rows * W * spp, (unsigned long long)counted.calls, secs);
+               (unsigned long long)rows * ncols * spp, (unsigned long long)counted.calls, secs);
   if (!accum_path.empty()) {
     FILE* f = std::fopen(accum_path.c_str(), "wb");
     std::fwrite(accum.data(), sizeof(double), accum.size(), f);

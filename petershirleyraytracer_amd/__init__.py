@@ -1,0 +1,17 @@
+"""MI355X-native path-tracing hot path of fengye/PeterShirleyRaytracer.
+
+The product is ``lib/libpsrt.so`` (HIP kernels for gfx950 behind the C ABI in
+``include/rt.h``) plus the C++ host (``csrc/host``, ``include/raytracer``).
+This Python package is host plumbing over that C ABI: scene/camera helpers,
+one-shot and device-resident renders, PPM output, and the multi-GPU sharding
+used by ``bench.py``. See DESIGN.md.
+"""
+from .render import (Context, camera_default, camera_look_at, device_count, params, ppm_p3,
+                     probe_f64, quantize, render, rows_owned, scene_random_spheres,
+                     scene_two_spheres, write_ppm)
+
+__all__ = [
+    "Context", "camera_default", "camera_look_at", "device_count", "params", "ppm_p3",
+    "probe_f64", "quantize", "render", "rows_owned", "scene_random_spheres",
+    "scene_two_spheres", "write_ppm",
+]

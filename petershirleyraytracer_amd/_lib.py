@@ -1,0 +1,106 @@
+"""ctypes binding of libpsrt.so (include/rt.h).
+
+The product path is the HIP library: if ``lib/libpsrt.so`` is missing or has
+no HIP device, calls raise — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from .build import LIB
+
+RT_OK = 0
+ERRORS = {-1: "RT_E_INVALID", -2: "RT_E_HIP", -3: "RT_E_NODEVICE", -4: "RT_E_NOMEM",
+          -5: "RT_E_SCENE"}
+
+# Every symbol include/rt.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "rt_rows_owned", "rt_render", "rt_quantize_ppm", "rt_context_create", "rt_context_destroy",
+    "rt_context_set_scene", "rt_render_device", "rt_context_sync_stats", "rt_quantize_device",
+    "rt_camera_default", "rt_camera_look_at", "rt_scene_two_spheres", "rt_scene_random_spheres",
+    "rt_last_error", "rt_abi_version", "rt_device_count", "rt_build_info", "rt_debug_probe_f64",
+    "rt_debug_world_hit",
+]
+
+
+class RtSphere(C.Structure):
+    _fields_ = [("cx", C.c_double), ("cy", C.c_double), ("cz", C.c_double), ("r", C.c_double)]
+
+
+class RtCamera(C.Structure):
+    _fields_ = [("origin", C.c_double * 3), ("lower_left", C.c_double * 3),
+                ("horizontal", C.c_double * 3), ("vertical", C.c_double * 3)]
+
+
+class RtParams(C.Structure):
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("spp", C.c_int),
+                ("max_depth", C.c_int), ("seed", C.c_uint64), ("row_offset", C.c_int),
+                ("row_stride", C.c_int), ("flags", C.c_uint)]
+
+
+class RtStats(C.Structure):
+    _fields_ = [("samples", C.c_uint64), ("rays", C.c_uint64), ("sphere_tests", C.c_uint64),
+                ("kernel_ms", C.c_double), ("total_ms", C.c_double)]
+
+
+class RtError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(build_if_missing: bool = False):
+    """Load libpsrt.so. Raises if it is absent (unless asked to build it)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB):
+        if build_if_missing:
+            from .build import build_lib
+            build_lib()
+        else:
+            raise RtError(f"libpsrt.so not built ({LIB}); run __graft_entry__.build() or "
+                          f"python -m petershirleyraytracer_amd.build")
+    L = C.CDLL(LIB)
+    P = C.POINTER
+    sig = {
+        "rt_rows_owned": ([C.c_int, C.c_int, C.c_int], C.c_int),
+        "rt_render": ([P(RtSphere), C.c_int, P(RtCamera), P(RtParams), P(C.c_double),
+                       P(C.c_ubyte), P(RtStats)], C.c_int),
+        "rt_quantize_ppm": ([P(C.c_double), C.c_int, C.c_int, C.c_int, P(C.c_ubyte)], C.c_int),
+        "rt_context_create": ([C.c_int, P(C.c_void_p)], C.c_int),
+        "rt_context_destroy": ([C.c_void_p], C.c_int),
+        "rt_context_set_scene": ([C.c_void_p, P(RtSphere), C.c_int, P(RtCamera)], C.c_int),
+        "rt_render_device": ([C.c_void_p, P(RtParams), C.c_void_p, C.c_void_p, C.c_void_p],
+                             C.c_int),
+        "rt_context_sync_stats": ([C.c_void_p, P(RtStats)], C.c_int),
+        "rt_quantize_device": ([C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                C.c_void_p], C.c_int),
+        "rt_camera_default": ([P(RtCamera)], C.c_int),
+        "rt_camera_look_at": ([P(C.c_double), P(C.c_double), P(C.c_double), C.c_double,
+                               C.c_double, P(RtCamera)], C.c_int),
+        "rt_scene_two_spheres": ([P(RtSphere), C.c_int], C.c_int),
+        "rt_scene_random_spheres": ([C.c_uint, P(RtSphere), C.c_int], C.c_int),
+        "rt_last_error": ([], C.c_char_p),
+        "rt_abi_version": ([], C.c_int),
+        "rt_device_count": ([], C.c_int),
+        "rt_build_info": ([], C.c_char_p),
+        "rt_debug_probe_f64": ([C.c_int, P(C.c_double), P(C.c_double), P(C.c_double), C.c_int],
+                               C.c_int),
+        "rt_debug_world_hit": ([P(RtSphere), C.c_int, P(C.c_double), C.c_int, P(C.c_double)],
+                               C.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != RT_OK:
+        msg = load().rt_last_error().decode(errors="replace")
+        raise RtError(f"{what} failed: {ERRORS.get(rc, rc)}: {msg}")

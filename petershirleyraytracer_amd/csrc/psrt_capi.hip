@@ -1,0 +1,433 @@
+// psrt_capi.hip — the C ABI of include/rt.h on HIP.
+//
+// Replaces the reference's pixel loop (main.cc:72-88) for a shard of rows:
+// the scene arrives flattened (rt_sphere[], rt_camera), device buffers are
+// owned by an rt_context, and one render enqueues, per sample chunk, one
+// psrt_trace megakernel launch and one psrt_reduce launch on a HIP stream.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rt.h"
+#include "psrt_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                  \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return fail(e_ == hipErrorOutOfMemory ? RT_E_NOMEM : RT_E_HIP, "%s: %s (%s:%d)", \
+                  #expr, hipGetErrorString(e_), __FILE__, __LINE__);                   \
+  } while (0)
+
+uint64_t splitmix64_host(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+size_t sample_buffer_cap_bytes() {
+  const char* e = std::getenv("PSRT_SAMPLE_BUF_MB");
+  size_t mb = e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)4096;
+  if (mb < 1) mb = 1;
+  return mb << 20;
+}
+
+}  // namespace
+
+struct rt_context {
+  int device = 0;
+  int cus = 0;
+  int grid = 0;
+  hipStream_t stream = nullptr;
+  double4* d_geo = nullptr;
+  double* d_inv_r = nullptr;
+  int n = -1;
+  int n_cap = 0;
+  rt_camera cam{};
+  double* d_samples = nullptr;
+  size_t samples_cap = 0;  // doubles
+  double* d_accum_tmp = nullptr;
+  size_t accum_tmp_cap = 0;  // doubles
+  unsigned long long* d_counters = nullptr;  // [0] work queue head, [1] rays
+  std::vector<hipEvent_t> ev;  // pairs around each trace launch
+  int ev_used = 0;
+  hipEvent_t ev_all0 = nullptr, ev_all1 = nullptr;
+  rt_stats last{};
+  int n_last = 0;
+};
+
+namespace {
+
+int ensure_events(rt_context* c, int pairs) {
+  while ((int)c->ev.size() < 2 * pairs) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreate(&e));
+    c->ev.push_back(e);
+  }
+  return RT_OK;
+}
+
+int ensure_buf(double** p, size_t* cap, size_t need) {
+  if (*cap >= need && *p) return RT_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  HIP_TRY(hipMalloc(p, need * sizeof(double)));
+  *cap = need;
+  return RT_OK;
+}
+
+std::mutex g_default_mu;
+rt_context* g_default[64] = {};
+
+int default_device() {
+  const char* e = std::getenv("RT_DEVICE");
+  return e ? std::atoi(e) : 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rt_last_error(void) { return g_err.c_str(); }
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+const char* rt_build_info(void) {
+  return "psrt gfx950 megakernel (fp64 exact, -ffp-contract=off); trace block " "256";
+}
+
+int rt_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int rt_rows_owned(int height, int row_offset, int row_stride) {
+  if (height <= 0 || row_stride <= 0 || row_offset < 0 || row_offset >= height) return 0;
+  return (height - 1 - row_offset) / row_stride + 1;
+}
+
+int rt_context_create(int device, rt_context** out) {
+  if (!out) return fail(RT_E_INVALID, "rt_context_create: out is NULL");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(RT_E_NODEVICE, "rt_context_create: no HIP device visible");
+  if (device < 0 || device >= ndev)
+    return fail(RT_E_INVALID, "rt_context_create: device %d out of range [0,%d)", device, ndev);
+  HIP_TRY(hipSetDevice(device));
+  rt_context* c = new rt_context();
+  c->device = device;
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  c->cus = prop.multiProcessorCount;
+  int per_cu = 0;
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace,
+                                                        psrt::kTraceBlock, 0));
+  if (per_cu < 1) per_cu = 1;
+  c->grid = c->cus * per_cu;
+  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIP_TRY(hipMalloc(&c->d_counters, 2 * sizeof(unsigned long long)));
+  HIP_TRY(hipEventCreate(&c->ev_all0));
+  HIP_TRY(hipEventCreate(&c->ev_all1));
+  *out = c;
+  return RT_OK;
+}
+
+int rt_context_destroy(rt_context* c) {
+  if (!c) return RT_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  (void)hipFree(c->d_geo);
+  (void)hipFree(c->d_inv_r);
+  (void)hipFree(c->d_samples);
+  (void)hipFree(c->d_accum_tmp);
+  (void)hipFree(c->d_counters);
+  for (auto e : c->ev) (void)hipEventDestroy(e);
+  if (c->ev_all0) (void)hipEventDestroy(c->ev_all0);
+  if (c->ev_all1) (void)hipEventDestroy(c->ev_all1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return RT_OK;
+}
+
+int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_camera* cam) {
+  if (!c || !cam || n < 0 || (n > 0 && !sph))
+    return fail(RT_E_INVALID, "rt_context_set_scene: bad arguments");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const int cap = n > 0 ? n : 1;
+  if (cap > c->n_cap) {
+    (void)hipFree(c->d_geo);
+    (void)hipFree(c->d_inv_r);
+    c->d_geo = nullptr;
+    c->d_inv_r = nullptr;
+    c->n_cap = 0;
+    HIP_TRY(hipMalloc(&c->d_geo, cap * sizeof(double4)));
+    HIP_TRY(hipMalloc(&c->d_inv_r, cap * sizeof(double)));
+    c->n_cap = cap;
+  }
+  // sphere.cc:11 radius*radius and vec3.h:151-154 1/t, each the same IEEE
+  // product/quotient the reference forms per call.
+  std::vector<double4> geo(cap);
+  std::vector<double> inv(cap);
+  for (int k = 0; k < n; ++k) {
+    geo[k] = make_double4(sph[k].cx, sph[k].cy, sph[k].cz, sph[k].r * sph[k].r);
+    inv[k] = 1 / sph[k].r;
+  }
+  if (n > 0) {
+    HIP_TRY(hipMemcpy(c->d_geo, geo.data(), n * sizeof(double4), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_inv_r, inv.data(), n * sizeof(double), hipMemcpyHostToDevice));
+  }
+  c->n = n;
+  c->cam = *cam;
+  return RT_OK;
+}
+
+static int check_params(const rt_params* p) {
+  if (!p) return fail(RT_E_INVALID, "params is NULL");
+  if (p->width < 2 || p->height < 2)
+    return fail(RT_E_INVALID, "width/height must be >= 2 (got %d x %d)", p->width, p->height);
+  if (p->spp < 1) return fail(RT_E_INVALID, "spp must be >= 1 (got %d)", p->spp);
+  if (p->max_depth < -1 || p->max_depth > 100000)
+    return fail(RT_E_INVALID, "max_depth out of range (got %d)", p->max_depth);
+  if (p->row_stride < 1 || p->row_offset < 0 || p->row_offset >= p->height)
+    return fail(RT_E_INVALID, "bad shard: row_offset %d row_stride %d height %d", p->row_offset,
+                p->row_stride, p->height);
+  if ((long long)p->width * p->height >= (1LL << 32))
+    return fail(RT_E_INVALID, "image too large for 32-bit pixel ids");
+  if (p->flags != 0) return fail(RT_E_INVALID, "flags must be 0 (got %u)", p->flags);
+  return RT_OK;
+}
+
+int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigned char* d_rgb8,
+                     void* stream_) {
+  if (!c) return fail(RT_E_INVALID, "rt_render_device: ctx is NULL");
+  int rc = check_params(p);
+  if (rc) return rc;
+  if (c->n < 0) return fail(RT_E_SCENE, "rt_render_device: no scene set");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = stream_ ? (hipStream_t)stream_ : c->stream;
+  const int rows = rt_rows_owned(p->height, p->row_offset, p->row_stride);
+  const size_t P = (size_t)rows * p->width;
+
+  // sample chunking: samples buffer holds s_chunk x P x 3 doubles, units < 2^32
+  size_t s_chunk = sample_buffer_cap_bytes() / (P * 3 * sizeof(double));
+  if (s_chunk < 1) s_chunk = 1;
+  if (s_chunk > (size_t)p->spp) s_chunk = p->spp;
+  while (s_chunk > 1 && P * s_chunk >= (1ULL << 32)) s_chunk /= 2;
+  if (P * s_chunk >= (1ULL << 32)) return fail(RT_E_INVALID, "shard too large");
+  const int nchunks = (int)((p->spp + s_chunk - 1) / s_chunk);
+  rc = ensure_buf(&c->d_samples, &c->samples_cap, s_chunk * P * 3);
+  if (rc) return rc;
+  double* acc = d_accum;
+  if (!acc && nchunks > 1) {
+    rc = ensure_buf(&c->d_accum_tmp, &c->accum_tmp_cap, P * 3);
+    if (rc) return rc;
+    acc = c->d_accum_tmp;
+  }
+  rc = ensure_events(c, nchunks);
+  if (rc) return rc;
+
+  psrt::TraceArgs ta{};
+  ta.n = c->n;
+  for (int k = 0; k < 3; ++k) {
+    ta.org[k] = c->cam.origin[k];
+    ta.llc[k] = c->cam.lower_left[k];
+    ta.hor[k] = c->cam.horizontal[k];
+    ta.ver[k] = c->cam.vertical[k];
+  }
+  ta.width = p->width;
+  ta.height = p->height;
+  ta.max_depth = p->max_depth;
+  ta.row_offset = p->row_offset;
+  ta.row_stride = p->row_stride;
+  ta.pixels = (unsigned)P;
+  ta.seedmix = splitmix64_host(p->seed);
+  ta.work_counter = c->d_counters;
+  ta.ray_counter = c->d_counters + 1;
+
+  HIP_TRY(hipMemsetAsync(c->d_counters + 1, 0, sizeof(unsigned long long), st));
+  HIP_TRY(hipEventRecord(c->ev_all0, st));
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const int s0 = (int)(ch * s_chunk);
+    const int sc = (int)std::min<size_t>(s_chunk, (size_t)(p->spp - s0));
+    ta.s_begin = s0;
+    ta.s_count = sc;
+    ta.total_units = (uint64_t)P * sc;
+    HIP_TRY(hipMemsetAsync(c->d_counters, 0, sizeof(unsigned long long), st));
+    HIP_TRY(hipEventRecord(c->ev[2 * ch], st));
+    hipLaunchKernelGGL(psrt::psrt_trace, dim3(c->grid), dim3(psrt::kTraceBlock), 0, st,
+                       (const double4*)c->d_geo, (const double*)c->d_inv_r, c->d_samples, ta);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev[2 * ch + 1], st));
+    psrt::ReduceArgs ra{};
+    ra.samples = c->d_samples;
+    ra.pixels = (unsigned)P;
+    ra.s_count = sc;
+    ra.first_chunk = ch == 0;
+    ra.spp_total = p->spp;
+    ra.accum = acc;
+    ra.rgb8 = (ch == nchunks - 1) ? d_rgb8 : nullptr;
+    const unsigned blocks = (unsigned)((P + 255) / 256);
+    hipLaunchKernelGGL(psrt::psrt_reduce, dim3(blocks), dim3(256), 0, st, ra);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipEventRecord(c->ev_all1, st));
+  c->ev_used = nchunks;
+  c->last = rt_stats{};
+  c->last.samples = (uint64_t)P * p->spp;
+  c->n_last = c->n;
+  return RT_OK;
+}
+
+int rt_context_sync_stats(rt_context* c, rt_stats* s) {
+  if (!c) return fail(RT_E_INVALID, "rt_context_sync_stats: ctx is NULL");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipEventSynchronize(c->ev_all1));
+  unsigned long long rays = 0;
+  HIP_TRY(hipMemcpy(&rays, c->d_counters + 1, sizeof rays, hipMemcpyDeviceToHost));
+  double kms = 0.0;
+  for (int ch = 0; ch < c->ev_used; ++ch) {
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev[2 * ch], c->ev[2 * ch + 1]));
+    kms += ms;
+  }
+  float all = 0.f;
+  HIP_TRY(hipEventElapsedTime(&all, c->ev_all0, c->ev_all1));
+  c->last.rays = rays;
+  c->last.sphere_tests = rays * (uint64_t)(c->n_last > 0 ? c->n_last : 0);
+  c->last.kernel_ms = kms;
+  c->last.total_ms = all;
+  if (s) *s = c->last;
+  return RT_OK;
+}
+
+int rt_quantize_device(rt_context* c, const double* d_accum, int width, int rows, int spp,
+                       unsigned char* d_rgb8, void* stream_) {
+  if (!c || !d_accum || !d_rgb8 || width <= 0 || rows < 0 || spp <= 0)
+    return fail(RT_E_INVALID, "rt_quantize_device: bad arguments");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = stream_ ? (hipStream_t)stream_ : c->stream;
+  const size_t n = (size_t)width * rows * 3;
+  if (n == 0) return RT_OK;
+  hipLaunchKernelGGL(psrt::psrt_quantize, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     d_accum, d_rgb8, (unsigned)n, spp);
+  HIP_TRY(hipGetLastError());
+  return RT_OK;
+}
+
+static int get_default_context(rt_context** out) {
+  std::lock_guard<std::mutex> lk(g_default_mu);
+  int dev = default_device();
+  if (dev < 0 || dev >= 64) return fail(RT_E_INVALID, "RT_DEVICE out of range");
+  if (!g_default[dev]) {
+    int rc = rt_context_create(dev, &g_default[dev]);
+    if (rc) return rc;
+  }
+  *out = g_default[dev];
+  return RT_OK;
+}
+
+int rt_render(const rt_sphere* sph, int n, const rt_camera* cam, const rt_params* p,
+              double* accum_rgb, unsigned char* rgb8, rt_stats* stats) {
+  if (!cam || !p || (!accum_rgb && !rgb8) || n < 0 || (n > 0 && !sph))
+    return fail(RT_E_INVALID, "rt_render: bad arguments");
+  int rc = check_params(p);
+  if (rc) return rc;
+  rt_context* c = nullptr;
+  rc = get_default_context(&c);
+  if (rc) return rc;
+  rc = rt_context_set_scene(c, sph, n, cam);
+  if (rc) return rc;
+  const int rows = rt_rows_owned(p->height, p->row_offset, p->row_stride);
+  const size_t P = (size_t)rows * p->width;
+  rc = ensure_buf(&c->d_accum_tmp, &c->accum_tmp_cap, P * 3 + (P * 3 + 7) / 8);
+  if (rc) return rc;
+  double* d_acc = c->d_accum_tmp;
+  unsigned char* d_rgb = (unsigned char*)(c->d_accum_tmp + P * 3);
+  rc = rt_render_device(c, p, d_acc, rgb8 ? d_rgb : nullptr, nullptr);
+  if (rc) return rc;
+  rc = rt_context_sync_stats(c, stats);
+  if (rc) return rc;
+  if (accum_rgb)
+    HIP_TRY(hipMemcpy(accum_rgb, d_acc, P * 3 * sizeof(double), hipMemcpyDeviceToHost));
+  if (rgb8) HIP_TRY(hipMemcpy(rgb8, d_rgb, P * 3, hipMemcpyDeviceToHost));
+  return RT_OK;
+}
+
+// Debug entry: run one f64 primitive on the device (numerics parity tests).
+int rt_debug_probe_f64(int op, const double* x, const double* y, double* out, int n) {
+  if (!x || !y || !out || n < 0) return fail(RT_E_INVALID, "rt_debug_probe_f64: bad arguments");
+  if (n == 0) return RT_OK;
+  rt_context* c = nullptr;
+  int rc = get_default_context(&c);
+  if (rc) return rc;
+  double *dx, *dy, *dout;
+  HIP_TRY(hipMalloc(&dx, n * sizeof(double)));
+  HIP_TRY(hipMalloc(&dy, n * sizeof(double)));
+  HIP_TRY(hipMalloc(&dout, n * sizeof(double)));
+  HIP_TRY(hipMemcpy(dx, x, n * sizeof(double), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dy, y, n * sizeof(double), hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(psrt::psrt_probe_f64, dim3((n + 255) / 256), dim3(256), 0, c->stream, op,
+                     (const double*)dx, (const double*)dy, dout, (unsigned)n);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMemcpy(out, dout, n * sizeof(double), hipMemcpyDeviceToHost));
+  (void)hipFree(dx);
+  (void)hipFree(dy);
+  (void)hipFree(dout);
+  return RT_OK;
+}
+
+// Debug entry: hittable_list::hit on the device for `count` rays
+// (rays[k] = {o, d, tmin, tmax}; out[k] = {index, p, normal, t, front_face}).
+int rt_debug_world_hit(const rt_sphere* sph, int n, const double* rays, int count, double* out) {
+  if (!rays || !out || count < 0 || n < 0 || (n > 0 && !sph))
+    return fail(RT_E_INVALID, "rt_debug_world_hit: bad arguments");
+  if (count == 0) return RT_OK;
+  rt_context* c = nullptr;
+  int rc = get_default_context(&c);
+  if (rc) return rc;
+  rt_camera cam{};
+  rc = rt_context_set_scene(c, sph, n, &cam);
+  if (rc) return rc;
+  double *dr, *dout;
+  HIP_TRY(hipMalloc(&dr, (size_t)count * 8 * sizeof(double)));
+  HIP_TRY(hipMalloc(&dout, (size_t)count * 9 * sizeof(double)));
+  HIP_TRY(hipMemcpy(dr, rays, (size_t)count * 8 * sizeof(double), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemset(dout, 0, (size_t)count * 9 * sizeof(double)));
+  hipLaunchKernelGGL(psrt::psrt_probe_hit, dim3((count + 63) / 64), dim3(64), 0, c->stream,
+                     (const double4*)c->d_geo, (const double*)c->d_inv_r, n, (const double*)dr,
+                     dout, (unsigned)count);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMemcpy(out, dout, (size_t)count * 9 * sizeof(double), hipMemcpyDeviceToHost));
+  (void)hipFree(dr);
+  (void)hipFree(dout);
+  return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,41 @@
+// psrt_device.h — device-side arithmetic of the hot path, in the reference's
+// IEEE binary64 operation order. Compiled with -ffp-contract=off: every
+// a*b+c below must stay a v_mul_f64 + v_add_f64 pair (an FMA changes the
+// rounding, flips trapped/escaped paths and biases the image; SURVEY.md
+// fact 5). Division and sqrt are the IEEE-correct gfx950 expansions.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace psrt {
+
+// ---- counter RNG (reference draw site random.h:4-14) --------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+// PCG32 XSH-RR step; returns the 31-bit value the reference's rand() yields.
+__device__ __forceinline__ uint32_t rand31(uint64_t& st) {
+  const uint64_t old = st;
+  st = old * 6364136223846793005ULL + 1442695040888963407ULL;
+  const uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
+  const uint32_t rot = (uint32_t)(old >> 59);
+  return ((xs >> rot) | (xs << ((32u - rot) & 31u))) >> 1;
+}
+
+// random_double(): (double)rand() / (RAND_MAX + 1.0). The divisor is 2^31, so
+// the quotient is exact and equals the product with 2^-31.
+__device__ __forceinline__ double random_double(uint64_t& st) {
+  return (double)rand31(st) * 0x1p-31;
+}
+
+// random_double(-1, 1) = -1 + (1 - -1) * random_double()   (random.h:10-14)
+__device__ __forceinline__ double random_pm1(uint64_t& st) {
+  return -1.0 + 2.0 * random_double(st);
+}
+
+}  // namespace psrt

@@ -1,0 +1,46 @@
+// psrt_kernels.h — launch arguments shared by the kernels and the C ABI host.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace psrt {
+
+constexpr int kTraceBlock = 256;     // 4 waves per workgroup
+constexpr unsigned kWorkChunk = 1024;  // units a wave takes per queue dequeue
+
+struct TraceArgs {
+  int n;               // spheres (geo: {cx, cy, cz, r*r}, inv_r: 1.0/r)
+  double org[3], llc[3], hor[3], ver[3];
+  int width, height, max_depth;
+  int row_offset, row_stride;
+  unsigned pixels;      // rows_owned * width
+  int s_begin, s_count; // sample chunk [s_begin, s_begin + s_count)
+  uint64_t total_units; // pixels * s_count  (< 2^32)
+  uint64_t seedmix;     // splitmix64(seed)
+  unsigned long long* work_counter;
+  unsigned long long* ray_counter;
+};
+
+struct ReduceArgs {
+  const double* samples;
+  unsigned pixels;
+  int s_count;
+  int first_chunk;
+  int spp_total;
+  double* accum;          // [pixels][3] (required unless single chunk + rgb only)
+  unsigned char* rgb8;    // [pixels][3] or nullptr (last chunk only)
+};
+
+__global__ void psrt_trace(const double4* __restrict__ geo, const double* __restrict__ inv_r,
+                           double* __restrict__ samples, TraceArgs a);
+__global__ void psrt_reduce(ReduceArgs a);
+__global__ void psrt_quantize(const double* __restrict__ accum, unsigned char* __restrict__ rgb8,
+                              unsigned n, int spp);
+__global__ void psrt_probe_hit(const double4* __restrict__ geo, const double* __restrict__ inv_r,
+                               int n, const double* __restrict__ rays, double* __restrict__ out,
+                               unsigned count);
+__global__ void psrt_probe_f64(int op, const double* __restrict__ x, const double* __restrict__ y,
+                               double* __restrict__ out, unsigned n);
+
+}  // namespace psrt

@@ -1,0 +1,320 @@
+// psrt_kernels.hip — gfx950 kernels of the path-tracing hot path.
+//
+//   psrt_trace    the megakernel: persistent lanes, one camera sample per
+//                 work unit, the ray_color recursion (main.cc:34-49) as a
+//                 bounce loop, hittable_list::hit / sphere::hit
+//                 (hittable_list.cc:3-20, sphere.cc:3-40) as a sweep over the
+//                 flattened sphere list, diffuse scatter (vec3.h:83-109).
+//                 A lane whose path ends stores that sample's colour and is
+//                 refilled from the wave's work window in the same iteration
+//                 (ballot + mbcnt), so every iteration every lane carries a
+//                 live ray until the queue drains.
+//   psrt_reduce   pixel_color += sample (main.cc:77-84) in sample order,
+//                 then write_color (color.h:8-24) on the last chunk.
+//
+// Data layout in HBM:
+//   geo[n]      double4 {cx, cy, cz, r*r}   sphere.cc:11 radius*radius
+//   inv_r[n]    double  1.0/r              vec3.h:151-154 (1/t)*v
+//   samples     double[s_count][P][3]      colour of sample s of pixel q
+//   accum       double[P][3]               P = rows_owned * W, reference order
+//   rgb8        uint8 [P][3]
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "psrt_device.h"
+#include "psrt_kernels.h"
+
+namespace psrt {
+
+__device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ unsigned mbcnt64(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
+// 0.5^k * x as the reference's k nested `0.5 * ray_color(...)` (main.cc:43).
+// x >= 0.5 here, so ldexp is exact (= the k products) while 2^-k*x stays
+// normal; past that the products are taken one by one as the reference does.
+__device__ __forceinline__ double half_pow(double x, int k) {
+  if (k <= 1000) return __builtin_ldexp(x, -k);
+  for (int m = 0; m < k; ++m) x = 0.5 * x;
+  return x;
+}
+
+// Sphere sweep of hittable_list::hit(r, tmin, tmax, rec) (hittable_list.cc:3-20
+// over sphere.cc:3-33). Only the winner's record is formed afterwards
+// (hit_record_of): every earlier accepted record is overwritten in the
+// reference, so the result is the same. Ties go to the later index
+// (sphere.cc:26 accepts t == tmax). NaN follows the reference: a NaN
+// discriminant is not "< 0" and a NaN root passes both range tests.
+__device__ __forceinline__ int sweep_linear(const double4* __restrict__ geo, int n, double ox,
+                                            double oy, double oz, double dx, double dy, double dz,
+                                            double A, double tmin, double tmax, double& best_t) {
+  int best_i = -1;
+  double closest = tmax;
+  for (int i = 0; i < n; ++i) {
+    const double4 s = geo[i];
+    const double ax = ox - s.x, ay = oy - s.y, az = oz - s.z;
+    const double hb = (dx * ax + dy * ay) + dz * az;
+    const double c = ((ax * ax + ay * ay) + az * az) - s.w;
+    const double disc = hb * hb - A * c;
+    if (!(disc < 0.0)) {
+      const double sq = __builtin_sqrt(disc);
+      double t = (-hb - sq) / A;
+      bool ok = true;
+      if (t < tmin || t > closest) {
+        t = (-hb + sq) / A;
+        if (t < tmin || t > closest) ok = false;
+      }
+      if (ok) {
+        closest = t;
+        best_i = i;
+      }
+    }
+  }
+  best_t = closest;
+  return best_i;
+}
+
+// sphere.cc:34-36 + hittable.h:14-18 for the winning sphere:
+// p = orig + dir*t (ray.h:25-28), outward = (p - c) / r = (1/r)*(p - c),
+// front_face = dot(dir, outward) < 0, normal flipped to face the ray.
+struct HitRec {
+  double px, py, pz, nx, ny, nz;
+  bool front;
+};
+
+__device__ __forceinline__ HitRec hit_record_of(const double4 s, double ir, double t, double ox,
+                                                double oy, double oz, double dx, double dy,
+                                                double dz) {
+  HitRec h;
+  h.px = ox + t * dx;
+  h.py = oy + t * dy;
+  h.pz = oz + t * dz;
+  h.nx = ir * (h.px - s.x);
+  h.ny = ir * (h.py - s.y);
+  h.nz = ir * (h.pz - s.z);
+  h.front = ((dx * h.nx + dy * h.ny) + dz * h.nz) < 0.0;
+  if (!h.front) h.nx = -h.nx, h.ny = -h.ny, h.nz = -h.nz;
+  return h;
+}
+
+__global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restrict__ geo,
+                                                          const double* __restrict__ inv_r,
+                                                          double* __restrict__ samples,
+                                                          TraceArgs a) {
+  const unsigned lane = lane_id();
+  const uint64_t total = a.total_units;
+
+  // wave-uniform work window
+  uint64_t win_base = 0;
+  unsigned win_left = 0;
+  bool exhausted = false;
+
+  bool active = false;
+  double ox = 0, oy = 0, oz = 0, dx = 0, dy = 0, dz = 0, A = 0;
+  int k = 0;          // bounces (hits) so far: current trace is at depth max_depth-k
+  uint64_t rng = 0;
+  unsigned q = 0;     // pixel index within the shard
+  unsigned sl = 0;    // sample index within the chunk
+  unsigned rays = 0;
+
+  for (;;) {
+    // ---- refill lanes whose sample finished (wavefront ballot compaction) ----
+    const bool need = !active;
+    const uint64_t need_mask = __ballot(need);
+    if (need_mask != 0 && !exhausted) {
+      const unsigned cnt = (unsigned)__popcll(need_mask);
+      const unsigned rank = mbcnt64(need_mask);
+      uint64_t nb = 0;
+      if (cnt > win_left) {
+        if (lane == 0) nb = atomicAdd(a.work_counter, (unsigned long long)kWorkChunk);
+        nb = __shfl(nb, 0);
+      }
+      if (need) {
+        const uint64_t unit = rank < win_left ? win_base + rank : nb + (rank - win_left);
+        if (unit < total) {  // total < 2^32 (host chunking)
+          q = (unsigned)unit / (unsigned)a.s_count;
+          sl = (unsigned)unit - q * (unsigned)a.s_count;
+          const unsigned row_k = q / (unsigned)a.width;
+          const unsigned i = q - row_k * (unsigned)a.width;
+          const int r = a.row_offset + (int)row_k * a.row_stride;
+          const int j = a.height - 1 - r;
+          const unsigned pix = (unsigned)j * (unsigned)a.width + i;
+          const unsigned s = (unsigned)a.s_begin + sl;
+          rng = splitmix64((((uint64_t)pix) << 32 | (uint64_t)s) ^ a.seedmix);
+          // main.cc:80-81, camera.h:25-28
+          const double u = ((double)i + random_double(rng)) / (double)(a.width - 1);
+          const double v = ((double)j + random_double(rng)) / (double)(a.height - 1);
+          ox = a.org[0], oy = a.org[1], oz = a.org[2];
+          dx = ((a.llc[0] + u * a.hor[0]) + v * a.ver[0]) - ox;
+          dy = ((a.llc[1] + u * a.hor[1]) + v * a.ver[1]) - oy;
+          dz = ((a.llc[2] + u * a.hor[2]) + v * a.ver[2]) - oz;
+          A = (dx * dx + dy * dy) + dz * dz;
+          k = 0;
+          active = true;
+        }
+      }
+      if (cnt > win_left) {  // the new window serves the overflow
+        win_base = nb + (cnt - win_left);
+        win_left = kWorkChunk - (cnt - win_left);
+      } else {
+        win_base += cnt;
+        win_left -= cnt;
+      }
+      if (win_base >= total) exhausted = true;
+    }
+    if (__ballot(active) == 0) break;
+
+    if (active) {
+      double col_r, col_g, col_b;
+      bool finish = false;
+      if (a.max_depth < 0) {  // main.cc:36-37 at the first call
+        col_r = col_g = col_b = 0.0;
+        finish = true;
+      } else {
+        ++rays;
+        double t;
+        const int hit =
+            sweep_linear(geo, a.n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), t);
+        if (hit >= 0) {
+          if (k >= a.max_depth) {  // depth 0 hit: 0.5 * ray_color(.., -1) = black
+            col_r = col_g = col_b = 0.0;
+            finish = true;
+          } else {
+            const HitRec h = hit_record_of(geo[hit], inv_r[hit], t, ox, oy, oz, dx, dy, dz);
+            const double px = h.px, py = h.py, pz = h.pz;
+            const double nx = h.nx, ny = h.ny, nz = h.nz;
+            // vec3.h:83-95 (g++ order: z, y, x) and vec3.h:102-109
+            double rx, ry, rz;
+            do {
+              rz = random_pm1(rng);
+              ry = random_pm1(rng);
+              rx = random_pm1(rng);
+            } while ((rx * rx + ry * ry) + rz * rz > 1.0);
+            if (!((rx * nx + ry * ny) + rz * nz > 0.0)) rx = -rx, ry = -ry, rz = -rz;
+            // main.cc:42-43: target = (p + n) + rv; ray(p, target - p)
+            dx = ((px + nx) + rx) - px;
+            dy = ((py + ny) + ry) - py;
+            dz = ((pz + nz) + rz) - pz;
+            ox = px, oy = py, oz = pz;
+            A = (dx * dx + dy * dy) + dz * dz;
+            ++k;
+          }
+        } else {
+          // main.cc:46-48, times 0.5^k (main.cc:43 unwound; exact)
+          const double y = (1.0 / __builtin_sqrt(A)) * dy;
+          const double tt = 0.5 * (y + 1.0);
+          const double w = 1.0 - tt;
+          col_r = half_pow(w + tt * 0.5, k);
+          col_g = half_pow(w + tt * 0.7, k);
+          col_b = half_pow(w + tt * 1.0, k);
+          finish = true;
+        }
+      }
+      if (finish) {
+        double* dst = samples + ((size_t)sl * a.pixels + q) * 3;
+        dst[0] = col_r;
+        dst[1] = col_g;
+        dst[2] = col_b;
+        active = false;
+      }
+    }
+  }
+
+  // rays traced by this wave -> one atomic
+  unsigned long long wr = rays;
+  for (int off = 32; off > 0; off >>= 1) wr += __shfl_xor(wr, off);
+  if (lane == 0 && wr) atomicAdd(a.ray_counter, wr);
+}
+
+// pixel_color += sample, in sample order (main.cc:77-84); write_color on the
+// last chunk (color.h:8-24).
+__global__ __launch_bounds__(256) void psrt_reduce(ReduceArgs a) {
+  const unsigned q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= a.pixels) return;
+  double r = 0.0, g = 0.0, b = 0.0;
+  if (!a.first_chunk) {
+    r = a.accum[(size_t)q * 3 + 0];
+    g = a.accum[(size_t)q * 3 + 1];
+    b = a.accum[(size_t)q * 3 + 2];
+  }
+  const double* src = a.samples + (size_t)q * 3;
+  const size_t stride = (size_t)a.pixels * 3;
+  for (int s = 0; s < a.s_count; ++s, src += stride) {
+    r += src[0];
+    g += src[1];
+    b += src[2];
+  }
+  if (a.accum) {
+    a.accum[(size_t)q * 3 + 0] = r;
+    a.accum[(size_t)q * 3 + 1] = g;
+    a.accum[(size_t)q * 3 + 2] = b;
+  }
+  if (a.rgb8) {
+    const double inv = 1.0 / (double)a.spp_total;
+    double c[3] = {r, g, b};
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      double x = __builtin_sqrt(c[ch] * inv);
+      x = (x < 0.0) ? 0.0 : x;  // std::max(x, 0.0)
+      x = (0.999 < x) ? 0.999 : x;  // std::min(x, 0.999)
+      a.rgb8[(size_t)q * 3 + ch] = (unsigned char)(int)(255.999 * x);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void psrt_quantize(const double* __restrict__ accum,
+                                                     unsigned char* __restrict__ rgb8,
+                                                     unsigned n, int spp) {
+  const unsigned e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  double x = __builtin_sqrt(accum[e] * (1.0 / (double)spp));
+  x = (x < 0.0) ? 0.0 : x;
+  x = (0.999 < x) ? 0.999 : x;
+  rgb8[e] = (unsigned char)(int)(255.999 * x);
+}
+
+// hittable_list::hit probe for known-answer tests: the same sweep and record
+// code as psrt_trace, one ray per thread. rays[k] = {ox,oy,oz,dx,dy,dz,tmin,tmax};
+// out[k] = {index, px, py, pz, nx, ny, nz, t, front_face}.
+__global__ void psrt_probe_hit(const double4* __restrict__ geo, const double* __restrict__ inv_r,
+                               int n, const double* __restrict__ rays, double* __restrict__ out,
+                               unsigned count) {
+  const unsigned k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  const double* r = rays + (size_t)k * 8;
+  const double ox = r[0], oy = r[1], oz = r[2], dx = r[3], dy = r[4], dz = r[5];
+  const double A = (dx * dx + dy * dy) + dz * dz;  // sphere.cc:9
+  double t;
+  const int i = sweep_linear(geo, n, ox, oy, oz, dx, dy, dz, A, r[6], r[7], t);
+  double* o = out + (size_t)k * 9;
+  o[0] = (double)i;
+  if (i >= 0) {
+    const HitRec h = hit_record_of(geo[i], inv_r[i], t, ox, oy, oz, dx, dy, dz);
+    o[1] = h.px, o[2] = h.py, o[3] = h.pz, o[4] = h.nx, o[5] = h.ny, o[6] = h.nz;
+    o[7] = t;
+    o[8] = h.front ? 1.0 : 0.0;
+  }
+}
+
+// Numerics probe: the f64 primitives the parity argument rests on.
+__global__ void psrt_probe_f64(int op, const double* __restrict__ x,
+                               const double* __restrict__ y, double* __restrict__ out,
+                               unsigned n) {
+  const unsigned e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  double r;
+  switch (op) {
+    case 0: r = __builtin_sqrt(x[e]); break;
+    case 1: r = x[e] / y[e]; break;
+    case 2: r = x[e] * y[e]; break;
+    case 3: r = x[e] + y[e]; break;
+    case 4: r = x[e] * y[e] + x[e]; break;  // must NOT contract
+    default: r = __builtin_ldexp(x[e], (int)y[e]); break;
+  }
+  out[e] = r;
+}
+
+}  // namespace psrt

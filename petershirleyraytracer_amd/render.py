@@ -1,0 +1,213 @@
+"""Host-side interface of the hot path (Python over the C ABI of include/rt.h).
+
+Mirrors the reference's pieces by name and meaning:
+
+* ``camera_default()``            camera() (camera.h:11-23)
+* ``camera_look_at(...)``         look-at pinhole extension for the final scene
+* ``scene_two_spheres()``         main.cc:61-63 world
+* ``scene_random_spheres(seed)``  final random-spheres world
+* ``render(...)``                 the main.cc:72-88 pixel loop for a shard of rows
+* ``write_ppm(...)``              main.cc:70 header + color.h:21-23 pixel lines
+
+Scenes are ``(n, 4)`` float64 arrays of (cx, cy, cz, r) in hittable_list order;
+cameras are ``(4, 3)`` float64 arrays (origin, lower_left, horizontal, vertical).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import RtCamera, RtParams, RtSphere, RtStats, check
+
+
+def _spheres(spheres) -> tuple:
+    arr = np.ascontiguousarray(np.asarray(spheres, dtype=np.float64).reshape(-1, 4))
+    buf = (RtSphere * max(1, len(arr)))()
+    if len(arr):
+        C.memmove(buf, arr.ctypes.data, arr.nbytes)
+    return buf, len(arr)
+
+
+def _camera(cam) -> RtCamera:
+    a = np.asarray(cam, dtype=np.float64).reshape(4, 3)
+    c = RtCamera()
+    for k in range(3):
+        c.origin[k], c.lower_left[k] = a[0, k], a[1, k]
+        c.horizontal[k], c.vertical[k] = a[2, k], a[3, k]
+    return c
+
+
+def _camera_array(c: RtCamera) -> np.ndarray:
+    return np.array([list(c.origin), list(c.lower_left), list(c.horizontal),
+                     list(c.vertical)], dtype=np.float64)
+
+
+def params(width: int, height: int, spp: int, max_depth: int = 50, seed: int = 0,
+           row_offset: int = 0, row_stride: int = 1) -> RtParams:
+    return RtParams(width, height, spp, max_depth, seed, row_offset, row_stride, 0)
+
+
+def rows_owned(height: int, row_offset: int = 0, row_stride: int = 1) -> int:
+    return _lib.load().rt_rows_owned(height, row_offset, row_stride)
+
+
+def camera_default() -> np.ndarray:
+    c = RtCamera()
+    check(_lib.load().rt_camera_default(C.byref(c)), "rt_camera_default")
+    return _camera_array(c)
+
+
+def camera_look_at(lookfrom=(13.0, 2.0, 3.0), lookat=(0.0, 0.0, 0.0), vup=(0.0, 1.0, 0.0),
+                   vfov: float = 20.0, aspect: float = 1.5) -> np.ndarray:
+    c = RtCamera()
+    d3 = C.c_double * 3
+    check(_lib.load().rt_camera_look_at(d3(*lookfrom), d3(*lookat), d3(*vup), vfov, aspect,
+                                        C.byref(c)), "rt_camera_look_at")
+    return _camera_array(c)
+
+
+def scene_two_spheres() -> np.ndarray:
+    buf = (RtSphere * 2)()
+    n = _lib.load().rt_scene_two_spheres(buf, 2)
+    return np.frombuffer(buf, dtype=np.float64, count=4 * n).reshape(n, 4).copy()
+
+
+def scene_random_spheres(seed: int = 1) -> np.ndarray:
+    L = _lib.load()
+    n = L.rt_scene_random_spheres(seed, None, 0)
+    buf = (RtSphere * n)()
+    L.rt_scene_random_spheres(seed, buf, n)
+    return np.frombuffer(buf, dtype=np.float64, count=4 * n).reshape(n, 4).copy()
+
+
+def stats_dict(s: RtStats) -> dict:
+    return dict(samples=s.samples, rays=s.rays, sphere_tests=s.sphere_tests,
+                kernel_ms=s.kernel_ms, total_ms=s.total_ms)
+
+
+def render(spheres, camera, width: int, height: int, spp: int, max_depth: int = 50,
+           seed: int = 0, row_offset: int = 0, row_stride: int = 1, want_rgb: bool = True):
+    """One-shot render of the owned rows on the default device (RT_DEVICE).
+
+    Returns (accum[rows, W, 3] float64, rgb8[rows, W, 3] uint8 or None, stats dict).
+    """
+    L = _lib.load()
+    sp, n = _spheres(spheres)
+    cam = _camera(camera)
+    p = params(width, height, spp, max_depth, seed, row_offset, row_stride)
+    rows = L.rt_rows_owned(height, row_offset, row_stride)
+    if rows <= 0:
+        raise _lib.RtError(f"shard owns no rows: height={height} offset={row_offset} "
+                           f"stride={row_stride}")
+    acc = np.zeros((rows, width, 3), dtype=np.float64)
+    rgb = np.zeros((rows, width, 3), dtype=np.uint8) if want_rgb else None
+    st = RtStats()
+    check(L.rt_render(sp, n, C.byref(cam), C.byref(p),
+                      acc.ctypes.data_as(C.POINTER(C.c_double)),
+                      rgb.ctypes.data_as(C.POINTER(C.c_ubyte)) if rgb is not None else None,
+                      C.byref(st)), "rt_render")
+    return acc, rgb, stats_dict(st)
+
+
+def quantize(accum: np.ndarray, spp: int) -> np.ndarray:
+    """write_color (color.h:8-24) on host accumulators."""
+    acc = np.ascontiguousarray(accum, dtype=np.float64)
+    out = np.zeros(acc.shape, dtype=np.uint8)
+    rows, w = acc.shape[0], acc.shape[1]
+    check(_lib.load().rt_quantize_ppm(acc.ctypes.data_as(C.POINTER(C.c_double)), w, rows, spp,
+                                      out.ctypes.data_as(C.POINTER(C.c_ubyte))),
+          "rt_quantize_ppm")
+    return out
+
+
+class Context:
+    """An rt_context on one HIP device: device-resident scene and buffers."""
+
+    def __init__(self, device: int = 0):
+        self._L = _lib.load()
+        h = C.c_void_p()
+        check(self._L.rt_context_create(device, C.byref(h)), "rt_context_create")
+        self.handle = h
+        self.device = device
+
+    def set_scene(self, spheres, camera) -> None:
+        sp, n = _spheres(spheres)
+        cam = _camera(camera)
+        check(self._L.rt_context_set_scene(self.handle, sp, n, C.byref(cam)),
+              "rt_context_set_scene")
+
+    def render_device(self, p: RtParams, d_accum: int = 0, d_rgb8: int = 0,
+                      stream: int = 0) -> None:
+        """Enqueue a render into device pointers (ints, e.g. tensor.data_ptr())."""
+        check(self._L.rt_render_device(self.handle, C.byref(p), d_accum or None,
+                                       d_rgb8 or None, stream or None), "rt_render_device")
+
+    def sync_stats(self) -> dict:
+        st = RtStats()
+        check(self._L.rt_context_sync_stats(self.handle, C.byref(st)), "rt_context_sync_stats")
+        return stats_dict(st)
+
+    def quantize_device(self, d_accum: int, width: int, rows: int, spp: int, d_rgb8: int,
+                        stream: int = 0) -> None:
+        check(self._L.rt_quantize_device(self.handle, d_accum, width, rows, spp, d_rgb8,
+                                         stream or None), "rt_quantize_device")
+
+    def close(self) -> None:
+        if self.handle:
+            self._L.rt_context_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def ppm_p3(rgb8: np.ndarray) -> bytes:
+    """P3 text exactly as main.cc:70 and color.h:21-23 write it."""
+    rows, w = rgb8.shape[0], rgb8.shape[1]
+    flat = np.asarray(rgb8, dtype=np.uint8).reshape(-1, 3)
+    body = "".join(f"{r} {g} {b}\n" for r, g, b in flat.tolist())
+    return f"P3\n{w} {rows}\n255\n{body}".encode()
+
+
+def write_ppm(path: str, rgb8: np.ndarray, binary: bool = False) -> None:
+    """Write P3 (reference format) or P6 (binary) PPM."""
+    rows, w = rgb8.shape[0], rgb8.shape[1]
+    with open(path, "wb") as f:
+        if binary:
+            f.write(f"P6\n{w} {rows}\n255\n".encode())
+            f.write(np.ascontiguousarray(rgb8, dtype=np.uint8).tobytes())
+        else:
+            f.write(ppm_p3(rgb8))
+
+
+def device_count() -> int:
+    return _lib.load().rt_device_count()
+
+
+def probe_f64(op: int, x: np.ndarray, y: Optional[np.ndarray] = None) -> np.ndarray:
+    """Run one binary64 primitive on the device (numerics tests)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(np.zeros_like(x) if y is None else y, dtype=np.float64)
+    out = np.zeros_like(x)
+    P = C.POINTER(C.c_double)
+    check(_lib.load().rt_debug_probe_f64(op, x.ctypes.data_as(P), y.ctypes.data_as(P),
+                                         out.ctypes.data_as(P), len(x)), "rt_debug_probe_f64")
+    return out
+
+
+def world_hit(spheres, rays: np.ndarray) -> np.ndarray:
+    """hittable_list::hit on the device for rays[k] = (o, d, tmin, tmax);
+    returns out[k] = (index, p, normal, t, front_face) (debug / KAT entry)."""
+    sp, n = _spheres(spheres)
+    r = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 8)
+    out = np.zeros((len(r), 9), dtype=np.float64)
+    P = C.POINTER(C.c_double)
+    check(_lib.load().rt_debug_world_hit(sp, n, r.ctypes.data_as(P), len(r),
+                                         out.ctypes.data_as(P)), "rt_debug_world_hit")
+    return out

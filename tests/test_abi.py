@@ -1,0 +1,125 @@
+"""The C-ABI boundary (include/rt.h) without a GPU: the library loads, exports
+every declared symbol, its host helpers agree with the oracle and the
+reference fixtures, and render calls fail loudly (no CPU fallback)."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, golden, have_gpu, unhex
+
+import petershirleyraytracer_amd as P
+from petershirleyraytracer_amd import _lib
+from petershirleyraytracer_amd.build import LIB
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "rt.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_built():
+    assert os.path.exists(LIB), "run __graft_entry__.build() first"
+
+
+def test_exports_every_declared_symbol():
+    L = C.CDLL(LIB)
+    decl = declared_symbols()
+    assert len(decl) >= 19
+    for name in decl:
+        assert hasattr(L, name), name
+    assert sorted(_lib.EXPORTS) == decl
+
+
+def test_abi_version_and_info():
+    L = _lib.load()
+    assert L.rt_abi_version() == 1
+    assert b"gfx950" in L.rt_build_info()
+
+
+def test_rows_owned():
+    assert P.rows_owned(800, 0, 1) == 800
+    assert P.rows_owned(800, 3, 8) == 100
+    assert P.rows_owned(801, 0, 8) == 101
+    assert P.rows_owned(5, 4, 8) == 1
+    assert P.rows_owned(5, 5, 8) == 0
+    assert P.rows_owned(5, 0, 0) == 0
+    for h in (1, 7, 225, 800):
+        for w in (1, 2, 3, 8):
+            assert sum(P.rows_owned(h, r, w) for r in range(w)) == h
+
+
+def test_cameras_match_reference_fixtures(oracle_mod):
+    two = golden("counter_two.json")
+    assert np.array_equal(P.camera_default(), np.array(unhex(two["camera"])))
+    fin = golden("counter_final.json")
+    assert np.array_equal(P.camera_look_at(aspect=1200 / 800),
+                          np.array(unhex(fin["camera_1200x800"])))
+    for c in fin["cases"]:
+        assert np.array_equal(P.camera_look_at(aspect=c["width"] / c["height"]),
+                              np.array(unhex(c["camera"])))
+    for aspect in (1.0, 16 / 9, 3840 / 2160, 0.5):
+        assert np.array_equal(P.camera_look_at(aspect=aspect),
+                              oracle_mod.camera_look_at(aspect=aspect))
+
+
+def test_scenes_match_reference(final_scene):
+    assert np.array_equal(P.scene_two_spheres(), np.array(unhex(golden("counter_two.json")["spheres"])))
+    assert np.array_equal(P.scene_random_spheres(1), final_scene)
+
+
+def test_scene_generator_tracks_glibc(oracle_mod):
+    for seed in (2, 99, 123456):
+        assert np.array_equal(P.scene_random_spheres(seed), oracle_mod.scene_random_spheres(seed))
+
+
+def test_host_quantize_matches_oracle(oracle_mod):
+    rng = np.random.default_rng(0)
+    acc = rng.uniform(0, 120, size=(17, 23, 3))
+    acc[0, 0] = [0.0, 100.0, 1e-30]
+    acc[1, 1] = [99.8001, 99.9, 1e9]
+    for spp in (1, 10, 100):
+        assert np.array_equal(P.quantize(acc, spp), oracle_mod.quantize(acc, spp))
+
+
+def test_ppm_p3_format(oracle_mod):
+    rgb = np.arange(2 * 3 * 3, dtype=np.uint8).reshape(2, 3, 3)
+    assert P.ppm_p3(rgb) == oracle_mod.ppm_p3(rgb)
+    assert P.ppm_p3(rgb).startswith(b"P3\n3 2\n255\n0 1 2\n")
+
+
+def test_bad_arguments_are_errors():
+    L = _lib.load()
+    cam = _lib.RtCamera()
+    p = P.params(1, 1, 1)
+    acc = (C.c_double * 3)()
+    assert L.rt_render(None, 0, C.byref(cam), C.byref(p), acc, None, None) == -1
+    assert b"width/height" in L.rt_last_error()
+    p = P.params(4, 4, 0)
+    assert L.rt_render(None, 0, C.byref(cam), C.byref(p), acc, None, None) == -1
+    p = P.params(4, 4, 1, row_offset=4)
+    assert L.rt_render(None, 0, C.byref(cam), C.byref(p), acc, None, None) == -1
+    assert L.rt_render(None, 0, None, C.byref(p), acc, None, None) == -1
+
+
+@pytest.mark.skipif(have_gpu(), reason="checks the no-device path")
+def test_render_without_device_fails_loudly():
+    with pytest.raises(_lib.RtError) as e:
+        P.render(P.scene_two_spheres(), P.camera_default(), 8, 4, 1)
+    assert "RT_E_NODEVICE" in str(e.value) or "RT_E_HIP" in str(e.value)
+    with pytest.raises(_lib.RtError):
+        P.Context(0)
+
+
+def test_product_does_not_import_oracle():
+    """The product package must not reach the checker."""
+    pkg = os.path.join(ROOT, "petershirleyraytracer_amd")
+    for dp, _, fs in os.walk(pkg):
+        for f in fs:
+            if f.endswith((".py", ".cpp", ".hip", ".h", ".cc")):
+                txt = open(os.path.join(dp, f)).read()
+                assert "import oracle" not in txt and "liboracle" not in txt, f
+                assert "oracle/" not in txt, f
