@@ -1,0 +1,108 @@
+// psrt/render.hpp — drop-in replacement for the reference pixel loop
+// (programs/main.cc:70-88) over the C ABI of include/rt.h.
+//
+//   hittable_list world;                        // built with the usual API
+//   world.add(make_shared<sphere>(point3(0,0,-1), 0.5));
+//   camera cam;
+//   psrt::frame f = psrt::render(world, cam, 400, 225, 100, 50);
+//   psrt::write_ppm(std::cout, f);               // P3, exactly main.cc:70 + write_color
+//
+// psrt::flatten walks world.objects (hittable_list.h:40) in order, recursing
+// into nested hittable_lists (a nested list's closest-hit scan is the same
+// scan continued, so flattening keeps hittable_list::hit's result) and
+// packing every sphere's (centre, radius) — any other hittable is an error.
+#pragma once
+
+#include <cstdint>
+#include <ostream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../rt.h"
+#include "rtweekend.hpp"
+
+namespace psrt {
+
+struct frame {
+  int width = 0, height = 0, rows = 0, spp = 0;
+  std::vector<double> accum;        // rows x width x 3, reference order (top row first)
+  std::vector<unsigned char> rgb8;  // write_color bytes
+  rt_stats stats{};
+};
+
+inline void flatten_into(const hittable_list& list, std::vector<rt_sphere>& out) {
+  for (const auto& obj : list.objects) {
+    if (const auto* s = dynamic_cast<const sphere*>(obj.get())) {
+      out.push_back(rt_sphere{s->centre.x(), s->centre.y(), s->centre.z(), s->radius});
+    } else if (const auto* l = dynamic_cast<const hittable_list*>(obj.get())) {
+      flatten_into(*l, out);
+    } else {
+      throw std::invalid_argument("psrt::flatten: only sphere and hittable_list are supported");
+    }
+  }
+}
+
+inline std::vector<rt_sphere> flatten(const hittable_list& world) {
+  std::vector<rt_sphere> out;
+  flatten_into(world, out);
+  return out;
+}
+
+inline rt_camera to_rt(const camera& cam) {
+  rt_camera c{};
+  for (int k = 0; k < 3; ++k) {
+    c.origin[k] = cam.origin[k];
+    c.lower_left[k] = cam.lower_left_corner[k];
+    c.horizontal[k] = cam.horizontal[k];
+    c.vertical[k] = cam.vertical[k];
+  }
+  return c;
+}
+
+inline void check(int rc, const char* what) {
+  if (rc != RT_OK) throw std::runtime_error(std::string(what) + ": " + rt_last_error());
+}
+
+// main.cc:72-88 for output rows row_offset, row_offset+row_stride, ...
+inline frame render(const hittable_list& world, const camera& cam, int width, int height,
+                    int spp, int max_depth, uint64_t seed = 0, int row_offset = 0,
+                    int row_stride = 1) {
+  const std::vector<rt_sphere> spheres = flatten(world);
+  const rt_camera c = to_rt(cam);
+  rt_params p{};
+  p.width = width;
+  p.height = height;
+  p.spp = spp;
+  p.max_depth = max_depth;
+  p.seed = seed;
+  p.row_offset = row_offset;
+  p.row_stride = row_stride;
+  frame f;
+  f.width = width;
+  f.height = height;
+  f.spp = spp;
+  f.rows = rt_rows_owned(height, row_offset, row_stride);
+  if (f.rows <= 0) throw std::invalid_argument("psrt::render: shard owns no rows");
+  f.accum.resize((size_t)f.rows * width * 3);
+  f.rgb8.resize((size_t)f.rows * width * 3);
+  check(rt_render(spheres.data(), (int)spheres.size(), &c, &p, f.accum.data(), f.rgb8.data(),
+                  &f.stats),
+        "rt_render");
+  return f;
+}
+
+// "P3\n<w> <rows>\n255\n" then one "r g b" line per pixel (main.cc:70, color.h:21-23)
+inline void write_ppm(std::ostream& out, const frame& f) {
+  out << "P3\n" << f.width << ' ' << f.rows << "\n255\n";
+  for (size_t k = 0; k < f.rgb8.size(); k += 3)
+    out << (int)f.rgb8[k] << ' ' << (int)f.rgb8[k + 1] << ' ' << (int)f.rgb8[k + 2] << '\n';
+}
+
+// P6 (binary) variant of the same image
+inline void write_ppm_binary(std::ostream& out, const frame& f) {
+  out << "P6\n" << f.width << ' ' << f.rows << "\n255\n";
+  out.write(reinterpret_cast<const char*>(f.rgb8.data()), (std::streamsize)f.rgb8.size());
+}
+
+}  // namespace psrt

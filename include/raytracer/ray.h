@@ -1,0 +1,4 @@
+// ray.h — name-compatible entry point for code written against the reference's
+// programs/ray.h; the whole host API lives in psrt/rtweekend.hpp.
+#pragma once
+#include "../psrt/rtweekend.hpp"

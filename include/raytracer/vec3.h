@@ -1,0 +1,4 @@
+// vec3.h — name-compatible entry point for code written against the reference's
+// programs/vec3.h; the whole host API lives in psrt/rtweekend.hpp.
+#pragma once
+#include "../psrt/rtweekend.hpp"

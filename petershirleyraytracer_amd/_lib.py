@@ -56,6 +56,14 @@ def load(build_if_missing: bool = False):
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: torch ships its own libamdhip64 (SONAME
+    # libamdhip64.so.7, NEEDed by torch as "libamdhip64.so"). Loaded first, it
+    # also satisfies libpsrt.so's NEEDED libamdhip64.so.7; loaded after ours,
+    # torch would map a second runtime that cannot see the GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB):
         if build_if_missing:
             from .build import build_lib

@@ -1,0 +1,120 @@
+// raytracer — the reference's main() (programs/main.cc:51-92) on the MI355X
+// hot path. The scene and camera are built with the reference API
+// (include/raytracer/*.h); the pixel loop (main.cc:72-88) is replaced by
+// psrt::render -> rt_render (include/rt.h) -> the gfx950 megakernel.
+//
+//   raytracer                       # main.cc as written: 400 wide, 16:9, 100 spp, depth 50
+//   raytracer --scene final --width 1200 --height 800 --spp 100 -o out.ppm
+//   raytracer --rows 1:8 ...        # one interleaved shard (rows 1, 9, 17, ...)
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <iostream>
+#include <string>
+
+#include "psrt/render.hpp"
+#include "raytracer/camera.h"
+#include "raytracer/color.h"
+#include "raytracer/hittable_list.h"
+#include "raytracer/sphere.h"
+
+namespace {
+
+// The final random-spheres world (diffuse-only), with the
+// reference API: glibc srand(seed), per cell a choose draw then x, z jitter.
+void random_spheres(hittable_list& world, unsigned seed) {
+  srand(seed);
+  world.add(make_shared<sphere>(point3(0, -1000, 0), 1000));
+  for (int a = -11; a < 11; a++) {
+    for (int b = -11; b < 11; b++) {
+      (void)random_double();  // choose_mat
+      const double cx = a + 0.9 * random_double();
+      const double cz = b + 0.9 * random_double();
+      const point3 centre(cx, 0.2, cz);
+      if ((centre - point3(4, 0.2, 0)).length() > 0.9) world.add(make_shared<sphere>(centre, 0.2));
+    }
+  }
+  world.add(make_shared<sphere>(point3(0, 1, 0), 1.0));
+  world.add(make_shared<sphere>(point3(-4, 1, 0), 1.0));
+  world.add(make_shared<sphere>(point3(4, 1, 0), 1.0));
+}
+
+int usage() {
+  std::fprintf(stderr,
+               "raytracer [--scene two|final] [--width W] [--height H] [--spp S] [--depth D]\n"
+               "          [--seed N] [--rows OFF:STRIDE] [-o FILE] [--p6] [--accum FILE]\n");
+  return 2;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  std::string scene = "two", out_path, accum_path;
+  int width = 400, height = -1, spp = 100, depth = 50, row_off = 0, row_stride = 1;
+  unsigned long long seed = 0;
+  bool p6 = false;
+  for (int a = 1; a < argc; ++a) {
+    const std::string k = argv[a];
+    auto val = [&]() -> const char* { return a + 1 < argc ? argv[++a] : nullptr; };
+    const char* v = nullptr;
+    if (k == "--p6") { p6 = true; continue; }
+    if (!(v = val())) return usage();
+    if (k == "--scene") scene = v;
+    else if (k == "--width") width = std::atoi(v);
+    else if (k == "--height") height = std::atoi(v);
+    else if (k == "--spp") spp = std::atoi(v);
+    else if (k == "--depth") depth = std::atoi(v);
+    else if (k == "--seed") seed = std::strtoull(v, nullptr, 10);
+    else if (k == "-o") out_path = v;
+    else if (k == "--accum") accum_path = v;
+    else if (k == "--rows") {
+      if (std::sscanf(v, "%d:%d", &row_off, &row_stride) != 2) return usage();
+    } else return usage();
+  }
+
+  // world + camera (main.cc:53-63)
+  hittable_list world;
+  camera cam;
+  if (scene == "two") {
+    if (height < 0) height = (int)(width / cam.aspect_ratio);
+    world.add(make_shared<sphere>(point3(0, 0, -1), 0.5));
+    world.add(make_shared<sphere>(point3(0, -100.5, 0), 100.0));
+  } else if (scene == "final") {
+    if (height < 0) height = (int)(width / 1.5);
+    random_spheres(world, 1);
+    cam = camera(point3(13, 2, 3), point3(0, 0, 0), vec3(0, 1, 0), 20.0, (double)width / height);
+  } else {
+    return usage();
+  }
+
+  try {
+    const auto t0 = std::chrono::steady_clock::now();
+    const psrt::frame f = psrt::render(world, cam, width, height, spp, depth, seed, row_off,
+                                       row_stride);
+    const double secs =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::ofstream file;
+    if (!out_path.empty()) file.open(out_path, std::ios::binary);
+    std::ostream& out = out_path.empty() ? std::cout : file;
+    if (p6)
+      psrt::write_ppm_binary(out, f);
+    else
+      psrt::write_ppm(out, f);
+    if (!accum_path.empty()) {
+      std::ofstream acc(accum_path, std::ios::binary);
+      acc.write(reinterpret_cast<const char*>(f.accum.data()),
+                (std::streamsize)(f.accum.size() * sizeof(double)));
+    }
+    std::fprintf(stderr,
+                 "{\"samples\": %llu, \"rays\": %llu, \"kernel_ms\": %.3f, \"wall_s\": %.4f, "
+                 "\"msamples_per_s\": %.3f}\n",
+                 (unsigned long long)f.stats.samples, (unsigned long long)f.stats.rays,
+                 f.stats.kernel_ms, secs, f.stats.samples / secs / 1e6);
+    std::cerr << "Done.\n";
+  } catch (const std::exception& e) {
+    std::cerr << "raytracer: " << e.what() << "\n";
+    return 1;
+  }
+  return 0;
+}
