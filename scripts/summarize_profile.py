@@ -1,0 +1,61 @@
+"""Summarise a rocprofv3 session (scripts/gpu_profile.sh output) into profiles/.
+
+    python scripts/summarize_profile.py gpurun_out/prof_c3 profiles/r01 c3
+
+Writes <dst>/kernel_stats_<cfg>.csv (the --stats summary as produced),
+<dst>/pmc_<cfg>.csv (per-dispatch counters of the psrt kernels) and
+profiles/pmc_<cfg>.json (per-launch HBM bytes + derived rates that bench.py
+reads for roofline.traffic). gfx950 corrections (MI355X_MICROARCH.md §HBM):
+FETCH_SIZE counts half the bytes of wide coalesced reads -> doubled; counters
+are in KiB; GRBM_GUI_ACTIVE sums the 8 XCDs.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+src, dst, cfg = sys.argv[1], sys.argv[2], sys.argv[3]
+os.makedirs(dst, exist_ok=True)
+stats = os.path.join(src, "trace", "run_kernel_stats.csv")
+shutil.copy(stats, os.path.join(dst, f"kernel_stats_{cfg}.csv"))
+rows = []
+for f in sorted(glob.glob(os.path.join(src, "pmc_*", "run_counter_collection.csv"))):
+    for r in csv.DictReader(open(f)):
+        if "psrt" in r["Kernel_Name"]:
+            rows.append(r)
+with open(os.path.join(dst, f"pmc_{cfg}.csv"), "w", newline="") as f:
+    keys = ["Kernel_Name", "Counter_Name", "Counter_Value", "Grid_Size", "Workgroup_Size",
+            "VGPR_Count", "SGPR_Count", "LDS_Block_Size", "Start_Timestamp", "End_Timestamp"]
+    w = csv.DictWriter(f, fieldnames=keys)
+    w.writeheader()
+    for r in rows:
+        w.writerow({k: r[k] for k in keys})
+c = {}
+for r in rows:
+    if "psrt_trace" in r["Kernel_Name"]:
+        c[r["Counter_Name"]] = float(r["Counter_Value"])
+        c.setdefault("_dur_ns", []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+dur = sorted(c.pop("_dur_ns"))[len(c.get("_dur_ns", [])) // 2] if "_dur_ns" in c else None
+avg = {}
+for line in csv.DictReader(open(stats)):
+    if "psrt_trace" in line["Name"]:
+        avg = dict(calls=int(line["Calls"]), average_ns=float(line["AverageNs"]))
+fetch = c.get("FETCH_SIZE", 0.0) * 1024 * 2
+write = c.get("WRITE_SIZE", 0.0) * 1024
+secs = avg.get("average_ns", 0) * 1e-9
+out = {
+    "kernel": "psrt_trace", "config": cfg, "kernel_stats": avg,
+    "hbm_bytes_per_launch": fetch + write,
+    "fetch_bytes_per_launch_x2": fetch, "write_bytes_per_launch": write,
+    "hbm_gbps": (fetch + write) / secs / 1e9 if secs else None,
+    "clock_ghz": c["GRBM_GUI_ACTIVE"] / 8 / secs / 1e9 if secs and "GRBM_GUI_ACTIVE" in c else None,
+    "counters": c,
+}
+if "SQ_INSTS_VALU" in c and "SQ_WAVES" in c:
+    out["valu_insts_per_wave"] = c["SQ_INSTS_VALU"] / c["SQ_WAVES"]
+json.dump(out, open(os.path.join(ROOT := os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                 "profiles", f"pmc_{cfg}.json"), "w"), indent=1)
+json.dump(out, open(os.path.join(dst, f"pmc_{cfg}.json"), "w"), indent=1)
+print(json.dumps({k: v for k, v in out.items() if k != "counters"}, indent=1))
