@@ -55,6 +55,7 @@ PEAK_HBM = 8.0e12
 # hoisted per ray, r*r per sphere: the same values) + 1 compare.
 OPS_PER_TEST = 23
 EXEC_OPS_PER_TEST = 18
+BOX_OPS_FP64_EQ = 7  # FP32 slab test: 6 FMA + 7 min/max + compare = 14 FP32 ops
 
 
 def parse():
@@ -70,6 +71,7 @@ def parse():
     ap.add_argument("--cpu-procs", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--save-ppm", default="")
+    ap.add_argument("--no-cull", action="store_true", help="force the linear sphere sweep")
     return ap.parse_args()
 
 
@@ -169,6 +171,7 @@ def main():
 
     import petershirleyraytracer_amd as P
     from petershirleyraytracer_amd.dist import gather_frame, rows_owned, shard
+    from petershirleyraytracer_amd.render import FLAG_NO_CULL
 
     torch.cuda.set_device(local)
     if world > 1:
@@ -180,7 +183,8 @@ def main():
     ctx.set_scene(spheres, cam)
     off, stride = shard(rank, world)
     rows = rows_owned(h, rank, world)
-    prm = P.params(w, h, spp, args.max_depth, args.seed, off, stride)
+    prm = P.params(w, h, spp, args.max_depth, args.seed, off, stride,
+                   FLAG_NO_CULL if args.no_cull else 0)
     dev = torch.device("cuda", local)
     acc = torch.zeros((rows, w, 3), dtype=torch.float64, device=dev)
     rgb = torch.zeros((h, w, 3), dtype=torch.uint8, device=dev) if rank == 0 else None
@@ -190,7 +194,7 @@ def main():
         if world > 1:
             dist.barrier()
 
-    kernel_ms, rays, elapsed = [], [], 0.0
+    kernel_ms, rays, executed, elapsed = [], [], [], 0.0
     frame = None
     for step in range(args.warmup + args.steps):
         if step == args.warmup:
@@ -210,6 +214,7 @@ def main():
         if step >= args.warmup:
             kernel_ms.append(st["kernel_ms"])
             rays.append(st["rays"])
+            executed.append((st["tests_executed"], st["box_tests"]))
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t0
@@ -225,12 +230,15 @@ def main():
         n = len(spheres)
         avg_ms = float(np.mean(kernel_ms))
         rays_launch = float(np.mean(rays))  # this rank's rays per launch
-        tests = rays_launch * n
-        # Executed sweep work: 17 FP64 ops + 1 compare per ray-sphere test
-        # (the reference's 23-op test minus the per-ray A = dot(d,d) and the
-        # per-sphere r*r, hoisted with identical values). That is the VALU
-        # work the hardware must issue, so frac is a true utilisation.
-        achieved = tests * EXEC_OPS_PER_TEST / (avg_ms * 1e-3)
+        tests = rays_launch * n  # sphere::hit calls of the reference algorithm
+        ex_tests = float(np.mean([e[0] for e in executed]))
+        ex_boxes = float(np.mean([e[1] for e in executed]))
+        # Executed VALU work of psrt_trace, in FP64-op slots: 18 per exact
+        # sphere test (17 FP64 ops + compare: the reference's 23-op test with A
+        # hoisted per ray and r*r per sphere, identical values) and 7 per FP32
+        # box test (14 FP32 ops at twice the FP64 rate). frac is utilisation.
+        ex_ops = ex_tests * EXEC_OPS_PER_TEST + ex_boxes * BOX_OPS_FP64_EQ
+        achieved = ex_ops / (avg_ms * 1e-3)
         ref_equiv = tests * OPS_PER_TEST / (avg_ms * 1e-3)
         # algorithmic HBM bytes of one psrt_trace launch: each sample's colour
         # written once (3 x 8 B); the 485 x 40 B sphere list is L2-resident
@@ -263,13 +271,18 @@ def main():
                 "kernel": "psrt_trace",
                 "avg_launch_ms": round(avg_ms, 3),
                 "rays_per_launch": int(rays_launch),
-                "sphere_tests_per_launch": int(tests),
-                "ops_per_test": EXEC_OPS_PER_TEST,
+                "reference_sphere_tests_per_launch": int(tests),
+                "executed_sphere_tests_per_launch": int(ex_tests),
+                "executed_box_tests_per_launch": int(ex_boxes),
+                "ops_per_sphere_test": EXEC_OPS_PER_TEST,
+                "ops_per_box_test_fp64_eq": BOX_OPS_FP64_EQ,
                 "reference_ops_per_test": OPS_PER_TEST,
                 "reference_equivalent_tflops": round(ref_equiv / 1e12, 4),
-                "note": ("FP64 VALU-issue bound (non-FMA op peak 256 CU x 64 lanes x 2.4 GHz); "
-                         "achieved = sphere tests (rays x spheres) x 18 executed ops / avg "
-                         "psrt_trace launch; shading ops not counted; HBM is ~1e-4 of peak"),
+                "culling": "off (linear sweep)" if (args.no_cull or ex_boxes == 0) else "bvh",
+                "note": ("VALU-issue bound (FP64 non-FMA op peak 256 CU x 64 lanes x 2.4 GHz); "
+                         "achieved = executed sphere tests x 18 + box tests x 7 (FP64-op slots) "
+                         "/ avg psrt_trace launch; shading, RNG and traversal control not "
+                         "counted; reference_equivalent = rays x spheres x 23 / launch"),
                 "hbm_algorithmic_bytes_per_launch": hbm_alg,
                 "hbm_frac": round(hbm_alg / (avg_ms * 1e-3) / PEAK_HBM, 6),
             },

@@ -71,8 +71,9 @@ typedef struct {
  * the reference's own random_double() mapping. See DESIGN.md §RNG. */
 #define RT_RNG_COUNTER 0
 
-/* flags (reserved; must be 0) */
+/* flags */
 #define RT_FLAG_NONE 0
+#define RT_FLAG_NO_CULL 1u /* force the linear sphere sweep (no BVH): same bits, slower */
 
 typedef struct {
   int width;      /* image_width  (main.cc:57)                              */
@@ -87,11 +88,13 @@ typedef struct {
 
 /* Counters of one render (all ranks' shards add up to the frame's). */
 typedef struct {
-  uint64_t samples;      /* camera samples traced                           */
-  uint64_t rays;         /* ray_color() invocations that called world.hit   */
-  uint64_t sphere_tests; /* sphere::hit evaluations implied = rays * n      */
-  double kernel_ms;      /* device time of the trace kernels (HIP events)   */
-  double total_ms;       /* wall time inside the call                       */
+  uint64_t samples;        /* camera samples traced                          */
+  uint64_t rays;           /* ray_color() invocations that called world.hit  */
+  uint64_t sphere_tests;   /* sphere::hit calls of the reference = rays * n  */
+  uint64_t tests_executed; /* FP64 sphere tests the device ran (culled)      */
+  uint64_t box_tests;      /* FP32 BVH box tests the device ran              */
+  double kernel_ms;        /* device time of the trace kernels (HIP events)  */
+  double total_ms;         /* device time of the whole render                */
 } rt_stats;
 
 /* Number of rows a shard owns. */
@@ -170,10 +173,12 @@ const char* rt_build_info(void);
 int rt_debug_probe_f64(int op, const double* x, const double* y, double* out, int n);
 
 /* Debug: hittable_list::hit (hittable_list.cc:3-20) on the device with the
- * megakernel's own sweep, one ray per thread. rays[k*8..] = {ox,oy,oz,dx,dy,dz,
- * tmin,tmax}; out[k*9..] = {index (-1 miss), px,py,pz, nx,ny,nz, t, front_face}. */
+ * megakernel's own code, one ray per thread. rays[k*8..] = {ox,oy,oz,dx,dy,dz,
+ * tmin,tmax}; out[k*9..] = {index (-1 miss), px,py,pz, nx,ny,nz, t, front_face}.
+ * cull != 0: rays with tmin == 0 and tmax == +inf (the trace kernel's call)
+ * go through the BVH path when the scene has one. */
 int rt_debug_world_hit(const rt_sphere* spheres, int n_spheres, const double* rays,
-                       int count, double* out);
+                       int count, double* out, int cull);
 
 #ifdef __cplusplus
 }

@@ -41,6 +41,7 @@ class RtParams(C.Structure):
 
 class RtStats(C.Structure):
     _fields_ = [("samples", C.c_uint64), ("rays", C.c_uint64), ("sphere_tests", C.c_uint64),
+                ("tests_executed", C.c_uint64), ("box_tests", C.c_uint64),
                 ("kernel_ms", C.c_double), ("total_ms", C.c_double)]
 
 
@@ -97,8 +98,8 @@ def load(build_if_missing: bool = False):
         "rt_build_info": ([], C.c_char_p),
         "rt_debug_probe_f64": ([C.c_int, P(C.c_double), P(C.c_double), P(C.c_double), C.c_int],
                                C.c_int),
-        "rt_debug_world_hit": ([P(RtSphere), C.c_int, P(C.c_double), C.c_int, P(C.c_double)],
-                               C.c_int),
+        "rt_debug_world_hit": ([P(RtSphere), C.c_int, P(C.c_double), C.c_int, P(C.c_double),
+                                C.c_int], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

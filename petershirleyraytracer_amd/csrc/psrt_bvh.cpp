@@ -1,0 +1,188 @@
+// psrt_bvh.cpp — host build of the exact-culling BVH (see psrt_bvh.h).
+#include "psrt_bvh.h"
+
+#include <algorithm>
+#include <cmath>
+#include <limits>
+
+namespace psrt {
+namespace {
+
+struct Box {
+  double lo[3] = {std::numeric_limits<double>::infinity(), std::numeric_limits<double>::infinity(),
+                  std::numeric_limits<double>::infinity()};
+  double hi[3] = {-std::numeric_limits<double>::infinity(),
+                  -std::numeric_limits<double>::infinity(),
+                  -std::numeric_limits<double>::infinity()};
+  void grow(const Box& b) {
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = std::min(lo[k], b.lo[k]);
+      hi[k] = std::max(hi[k], b.hi[k]);
+    }
+  }
+  void grow(const double p[3]) {
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = std::min(lo[k], p[k]);
+      hi[k] = std::max(hi[k], p[k]);
+    }
+  }
+  double area() const {
+    const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    if (!(dx >= 0)) return 0.0;
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+  }
+};
+
+struct Prim {
+  Box box;
+  double c[3];
+  int32_t idx;
+};
+
+// float rounding toward -inf / +inf of a double
+float down(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+  return f;
+}
+float up(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+  return f;
+}
+
+struct Builder {
+  std::vector<Prim>& prims;
+  BvhHost& out;
+
+  // emit the subtree over prims[b, e) in DFS order; returns its node index
+  int build(int b, int e, int depth) {
+    out.depth = std::max(out.depth, depth);
+    Box bounds, cbox;
+    for (int i = b; i < e; ++i) {
+      bounds.grow(prims[i].box);
+      cbox.grow(prims[i].c);
+    }
+    const int me = (int)out.nodes.size();
+    out.nodes.push_back(BvhNode{});
+    BvhNode& nd0 = out.nodes[me];
+    for (int k = 0; k < 3; ++k) {
+      nd0.lo[k] = down(bounds.lo[k]);
+      nd0.hi[k] = up(bounds.hi[k]);
+    }
+    const int count = e - b;
+    int split = -1;
+    if (count > kLeafMax) split = sah_split(b, e, cbox, bounds);
+    if (split < 0) {
+      out.nodes[me].leaf = ((int32_t)out.leaf_idx.size() << 8) | count;
+      for (int i = b; i < e; ++i) out.leaf_idx.push_back(prims[i].idx);
+    } else {
+      out.nodes[me].leaf = -1;
+      build(b, split, depth + 1);
+      build(split, e, depth + 1);
+    }
+    out.nodes[me].skip = (int32_t)out.nodes.size();
+    return me;
+  }
+
+  // binned SAH on the widest centroid axis; -1 = make a leaf
+  int sah_split(int b, int e, const Box& cbox, const Box& bounds) {
+    int axis = 0;
+    double ext = -1;
+    for (int k = 0; k < 3; ++k)
+      if (cbox.hi[k] - cbox.lo[k] > ext) ext = cbox.hi[k] - cbox.lo[k], axis = k;
+    const int count = e - b;
+    if (!(ext > 0)) {  // coincident centroids: split by count
+      return count > 255 ? b + count / 2 : (count > kLeafMax ? b + count / 2 : -1);
+    }
+    constexpr int kBins = 16;
+    Box bb[kBins];
+    int bc[kBins] = {0};
+    auto bin_of = [&](const Prim& p) {
+      int i = (int)((p.c[axis] - cbox.lo[axis]) / ext * kBins);
+      return std::min(kBins - 1, std::max(0, i));
+    };
+    for (int i = b; i < e; ++i) {
+      const int k = bin_of(prims[i]);
+      bb[k].grow(prims[i].box);
+      ++bc[k];
+    }
+    double best = std::numeric_limits<double>::infinity();
+    int best_k = -1;
+    for (int k = 1; k < kBins; ++k) {
+      Box l, r;
+      int nl = 0, nr = 0;
+      for (int j = 0; j < k; ++j)
+        if (bc[j]) l.grow(bb[j]), nl += bc[j];
+      for (int j = k; j < kBins; ++j)
+        if (bc[j]) r.grow(bb[j]), nr += bc[j];
+      if (!nl || !nr) continue;
+      const double cost = l.area() * nl + r.area() * nr;
+      if (cost < best) best = cost, best_k = k;
+    }
+    if (best_k < 0) return b + count / 2;  // all in one bin: split by count
+    // cost model: traversal 1, intersection 2 (fp64 test ~ 2 fp32 box tests)
+    const double leaf_cost = 2.0 * count;
+    const double split_cost = 1.0 + 2.0 * best / std::max(bounds.area(), 1e-300);
+    if (count <= 4 && leaf_cost <= split_cost) return -1;
+    auto mid = std::partition(prims.begin() + b, prims.begin() + e,
+                              [&](const Prim& p) { return bin_of(p) < best_k; });
+    int m = (int)(mid - prims.begin());
+    if (m == b || m == e) m = b + count / 2;
+    return m;
+  }
+};
+
+}  // namespace
+
+BvhHost build_bvh(const rt_sphere* s, int n) {
+  BvhHost out;
+  if (n < kBvhMinSpheres || !s) return out;
+  std::vector<double> radii;
+  radii.reserve(n);
+  double scale = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double v[4] = {s[i].cx, s[i].cy, s[i].cz, s[i].r};
+    for (double x : v)
+      if (!std::isfinite(x) || std::fabs(x) > 1e6) return out;  // degenerate: linear sweep
+    radii.push_back(std::fabs(s[i].r));
+  }
+  std::vector<double> sorted = radii;
+  std::nth_element(sorted.begin(), sorted.begin() + n / 2, sorted.end());
+  const double median = sorted[n / 2];
+  std::vector<Prim> prims;
+  for (int i = 0; i < n; ++i) {
+    if (radii[i] > kBigRatio * median && radii[i] > 0) {
+      out.big_idx.push_back(i);
+      continue;
+    }
+    const double c[3] = {s[i].cx, s[i].cy, s[i].cz};
+    for (int k = 0; k < 3; ++k) scale = std::max(scale, std::fabs(c[k]) + radii[i]);
+  }
+  if ((int)out.big_idx.size() == n) return out;
+  // pad = 2^-13 S (S = max |c| + r over the BVH spheres). Error budget
+  // (DESIGN.md §8): the FP32 slab test's spatial error along an axis is
+  // <= 2^-24 (5|o| + 4S) (origin and direction rounding, one subtract, one
+  // multiply, the rounded-up tmax); the FP64 root error is ~1e-12. At
+  // |o|_inf <= 64 S that is <= 2^-15.6 S, >6x inside the pad.
+  scale = std::max(scale, 1.0);
+  out.pad = std::ldexp(scale, -13);
+  out.r_check = 64.0 * scale;
+  for (int i = 0; i < n; ++i) {
+    if (std::find(out.big_idx.begin(), out.big_idx.end(), i) != out.big_idx.end()) continue;
+    Prim p;
+    p.idx = i;
+    p.c[0] = s[i].cx, p.c[1] = s[i].cy, p.c[2] = s[i].cz;
+    for (int k = 0; k < 3; ++k) {
+      p.box.lo[k] = p.c[k] - radii[i] - out.pad;
+      p.box.hi[k] = p.c[k] + radii[i] + out.pad;
+    }
+    prims.push_back(p);
+  }
+  Builder bld{prims, out};
+  bld.build(0, (int)prims.size(), 0);
+  out.enabled = true;
+  return out;
+}
+
+}  // namespace psrt

@@ -1,0 +1,51 @@
+// psrt_bvh.h — exact culling structure for hittable_list::hit.
+//
+// A binary BVH over the scene's "small" spheres, laid out depth-first with a
+// skip link per node so the device walks it without a stack: on a box hit go
+// to node+1 (first child), on a miss — or after a leaf — go to `skip`.
+// "Big" spheres (radius > kBigRatio x the median radius, e.g. the r=1000
+// ground) would bloat every box; they are tested on every ray instead.
+//
+// Boxes are the spheres' bounds padded by `pad` (absolute) and rounded
+// outward to float. `pad` exceeds, with a wide margin, both the FP64 error of
+// a computed root (the point o + t*d of any accepted root lies within ~1e-12
+// of its sphere) and the FP32 slab-test error for ray origins with
+// |o|_inf <= r_check; rays outside that range take the exact linear sweep.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "../../include/rt.h"
+
+namespace psrt {
+
+// 32 bytes: read as two float4 on the device.
+struct BvhNode {
+  float lo[3];
+  int32_t skip;  // next node when this subtree is done/missed (== node count: end)
+  float hi[3];
+  int32_t leaf;  // -1 interior; else first << 8 | count (count <= 255)
+};
+static_assert(sizeof(BvhNode) == 32, "node layout");
+
+constexpr int kBvhMinSpheres = 17;   // below this the linear sweep wins
+constexpr double kBigRatio = 16.0;   // radius > 16 x median -> tested every ray
+constexpr int kLeafMax = 2;
+
+struct BvhHost {
+  std::vector<BvhNode> nodes;
+  std::vector<int32_t> leaf_idx;  // original sphere index per leaf slot
+  std::vector<int32_t> big_idx;   // original indices tested on every ray
+  double pad = 0.0;               // absolute box padding
+  double r_check = 0.0;           // rays with |o|_inf > r_check use the linear sweep
+  int depth = 0;
+  bool enabled = false;
+};
+
+// Builds the structure; enabled = false when the scene is too small or
+// degenerate (non-finite or non-positive radii, huge coordinates), in which
+// case the device uses the linear sweep for every ray.
+BvhHost build_bvh(const rt_sphere* spheres, int n);
+
+}  // namespace psrt

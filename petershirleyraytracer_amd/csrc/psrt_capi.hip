@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/rt.h"
+#include "psrt_bvh.h"
 #include "psrt_kernels.h"
 
 namespace {
@@ -59,7 +60,16 @@ size_t sample_buffer_cap_bytes() {
 struct rt_context {
   int device = 0;
   int cus = 0;
-  int grid = 0;
+  int grid = 0;       // resident blocks of psrt_trace<false>
+  int grid_bvh = 0;   // resident blocks of psrt_trace<true>
+  // exact-culling structure (psrt_bvh.h)
+  bool bvh = false;
+  float4* d_nodes = nullptr;
+  double4* d_leaf_geo = nullptr;
+  int* d_leaf_idx = nullptr;
+  int* d_big = nullptr;
+  int n_nodes = 0, n_big = 0, n_leaf = 0;
+  double r_check = 0.0;
   hipStream_t stream = nullptr;
   double4* d_geo = nullptr;
   double* d_inv_r = nullptr;
@@ -70,7 +80,7 @@ struct rt_context {
   size_t samples_cap = 0;  // doubles
   double* d_accum_tmp = nullptr;
   size_t accum_tmp_cap = 0;  // doubles
-  unsigned long long* d_counters = nullptr;  // [0] work queue head, [1] rays
+  unsigned long long* d_counters = nullptr;  // [0] queue head, [1] rays, [2] tests, [3] boxes
   std::vector<hipEvent_t> ev;  // pairs around each trace launch
   int ev_used = 0;
   hipEvent_t ev_all0 = nullptr, ev_all1 = nullptr;
@@ -144,12 +154,14 @@ int rt_context_create(int device, rt_context** out) {
   HIP_TRY(hipGetDeviceProperties(&prop, device));
   c->cus = prop.multiProcessorCount;
   int per_cu = 0;
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace,
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace<false>,
                                                         psrt::kTraceBlock, 0));
-  if (per_cu < 1) per_cu = 1;
-  c->grid = c->cus * per_cu;
+  c->grid = c->cus * (per_cu < 1 ? 1 : per_cu);
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace<true>,
+                                                        psrt::kTraceBlock, 0));
+  c->grid_bvh = c->cus * (per_cu < 1 ? 1 : per_cu);
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  HIP_TRY(hipMalloc(&c->d_counters, 2 * sizeof(unsigned long long)));
+  HIP_TRY(hipMalloc(&c->d_counters, 4 * sizeof(unsigned long long)));
   HIP_TRY(hipEventCreate(&c->ev_all0));
   HIP_TRY(hipEventCreate(&c->ev_all1));
   *out = c;
@@ -165,6 +177,10 @@ int rt_context_destroy(rt_context* c) {
   (void)hipFree(c->d_samples);
   (void)hipFree(c->d_accum_tmp);
   (void)hipFree(c->d_counters);
+  (void)hipFree(c->d_nodes);
+  (void)hipFree(c->d_leaf_geo);
+  (void)hipFree(c->d_leaf_idx);
+  (void)hipFree(c->d_big);
   for (auto e : c->ev) (void)hipEventDestroy(e);
   if (c->ev_all0) (void)hipEventDestroy(c->ev_all0);
   if (c->ev_all1) (void)hipEventDestroy(c->ev_all1);
@@ -203,7 +219,49 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
   }
   c->n = n;
   c->cam = *cam;
+  // exact culling structure
+  const psrt::BvhHost b = psrt::build_bvh(sph, n);
+  (void)hipFree(c->d_nodes);
+  (void)hipFree(c->d_leaf_geo);
+  (void)hipFree(c->d_leaf_idx);
+  (void)hipFree(c->d_big);
+  c->d_nodes = nullptr, c->d_leaf_geo = nullptr, c->d_leaf_idx = nullptr, c->d_big = nullptr;
+  c->bvh = b.enabled;
+  c->n_nodes = c->n_big = c->n_leaf = 0;
+  if (b.enabled) {
+    c->n_nodes = (int)b.nodes.size();
+    c->n_big = (int)b.big_idx.size();
+    c->n_leaf = (int)b.leaf_idx.size();
+    c->r_check = b.r_check;
+    std::vector<double4> lg(c->n_leaf);
+    for (int k = 0; k < c->n_leaf; ++k) lg[k] = geo[b.leaf_idx[k]];
+    HIP_TRY(hipMalloc(&c->d_nodes, b.nodes.size() * sizeof(psrt::BvhNode)));
+    HIP_TRY(hipMalloc(&c->d_leaf_geo, (size_t)c->n_leaf * sizeof(double4)));
+    HIP_TRY(hipMalloc(&c->d_leaf_idx, (size_t)c->n_leaf * sizeof(int)));
+    HIP_TRY(hipMalloc(&c->d_big, (size_t)(c->n_big > 0 ? c->n_big : 1) * sizeof(int)));
+    HIP_TRY(hipMemcpy(c->d_nodes, b.nodes.data(), b.nodes.size() * sizeof(psrt::BvhNode),
+                      hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_leaf_geo, lg.data(), lg.size() * sizeof(double4),
+                      hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_leaf_idx, b.leaf_idx.data(), b.leaf_idx.size() * sizeof(int),
+                      hipMemcpyHostToDevice));
+    if (c->n_big > 0)
+      HIP_TRY(hipMemcpy(c->d_big, b.big_idx.data(), b.big_idx.size() * sizeof(int),
+                        hipMemcpyHostToDevice));
+  }
   return RT_OK;
+}
+
+static psrt::BvhView bvh_view(const rt_context* c) {
+  psrt::BvhView v{};
+  v.nodes = c->d_nodes;
+  v.leaf_geo = c->d_leaf_geo;
+  v.leaf_idx = c->d_leaf_idx;
+  v.big_idx = c->d_big;
+  v.n_nodes = c->n_nodes;
+  v.n_big = c->n_big;
+  v.r_check = c->r_check;
+  return v;
 }
 
 static int check_params(const rt_params* p) {
@@ -218,7 +276,7 @@ static int check_params(const rt_params* p) {
                 p->row_stride, p->height);
   if ((long long)p->width * p->height >= (1LL << 32))
     return fail(RT_E_INVALID, "image too large for 32-bit pixel ids");
-  if (p->flags != 0) return fail(RT_E_INVALID, "flags must be 0 (got %u)", p->flags);
+  if (p->flags & ~RT_FLAG_NO_CULL) return fail(RT_E_INVALID, "unknown flags 0x%x", p->flags);
   return RT_OK;
 }
 
@@ -269,7 +327,9 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   ta.work_counter = c->d_counters;
   ta.ray_counter = c->d_counters + 1;
 
-  HIP_TRY(hipMemsetAsync(c->d_counters + 1, 0, sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(c->d_counters + 1, 0, 3 * sizeof(unsigned long long), st));
+  const bool use_bvh = c->bvh && !(p->flags & RT_FLAG_NO_CULL);
+  const psrt::BvhView bv = bvh_view(c);
   HIP_TRY(hipEventRecord(c->ev_all0, st));
   for (int ch = 0; ch < nchunks; ++ch) {
     const int s0 = (int)(ch * s_chunk);
@@ -279,8 +339,14 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     ta.total_units = (uint64_t)P * sc;
     HIP_TRY(hipMemsetAsync(c->d_counters, 0, sizeof(unsigned long long), st));
     HIP_TRY(hipEventRecord(c->ev[2 * ch], st));
-    hipLaunchKernelGGL(psrt::psrt_trace, dim3(c->grid), dim3(psrt::kTraceBlock), 0, st,
-                       (const double4*)c->d_geo, (const double*)c->d_inv_r, c->d_samples, ta);
+    if (use_bvh)
+      hipLaunchKernelGGL(psrt::psrt_trace<true>, dim3(c->grid_bvh), dim3(psrt::kTraceBlock), 0,
+                         st, (const double4*)c->d_geo, (const double*)c->d_inv_r, c->d_samples,
+                         ta, bv);
+    else
+      hipLaunchKernelGGL(psrt::psrt_trace<false>, dim3(c->grid), dim3(psrt::kTraceBlock), 0, st,
+                         (const double4*)c->d_geo, (const double*)c->d_inv_r, c->d_samples, ta,
+                         bv);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[2 * ch + 1], st));
     psrt::ReduceArgs ra{};
@@ -307,8 +373,9 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   if (!c) return fail(RT_E_INVALID, "rt_context_sync_stats: ctx is NULL");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipEventSynchronize(c->ev_all1));
-  unsigned long long rays = 0;
-  HIP_TRY(hipMemcpy(&rays, c->d_counters + 1, sizeof rays, hipMemcpyDeviceToHost));
+  unsigned long long cnt[3] = {0, 0, 0};
+  HIP_TRY(hipMemcpy(cnt, c->d_counters + 1, sizeof cnt, hipMemcpyDeviceToHost));
+  const unsigned long long rays = cnt[0];
   double kms = 0.0;
   for (int ch = 0; ch < c->ev_used; ++ch) {
     float ms = 0.f;
@@ -319,6 +386,8 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   HIP_TRY(hipEventElapsedTime(&all, c->ev_all0, c->ev_all1));
   c->last.rays = rays;
   c->last.sphere_tests = rays * (uint64_t)(c->n_last > 0 ? c->n_last : 0);
+  c->last.tests_executed = cnt[1];
+  c->last.box_tests = cnt[2];
   c->last.kernel_ms = kms;
   c->last.total_ms = all;
   if (s) *s = c->last;
@@ -404,7 +473,8 @@ int rt_debug_probe_f64(int op, const double* x, const double* y, double* out, in
 
 // Debug entry: hittable_list::hit on the device for `count` rays
 // (rays[k] = {o, d, tmin, tmax}; out[k] = {index, p, normal, t, front_face}).
-int rt_debug_world_hit(const rt_sphere* sph, int n, const double* rays, int count, double* out) {
+int rt_debug_world_hit(const rt_sphere* sph, int n, const double* rays, int count, double* out,
+                       int cull) {
   if (!rays || !out || count < 0 || n < 0 || (n > 0 && !sph))
     return fail(RT_E_INVALID, "rt_debug_world_hit: bad arguments");
   if (count == 0) return RT_OK;
@@ -421,7 +491,7 @@ int rt_debug_world_hit(const rt_sphere* sph, int n, const double* rays, int coun
   HIP_TRY(hipMemset(dout, 0, (size_t)count * 9 * sizeof(double)));
   hipLaunchKernelGGL(psrt::psrt_probe_hit, dim3((count + 63) / 64), dim3(64), 0, c->stream,
                      (const double4*)c->d_geo, (const double*)c->d_inv_r, n, (const double*)dr,
-                     dout, (unsigned)count);
+                     dout, (unsigned)count, bvh_view(c), (cull && c->bvh) ? 1 : 0);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipMemcpy(out, dout, (size_t)count * 9 * sizeof(double), hipMemcpyDeviceToHost));

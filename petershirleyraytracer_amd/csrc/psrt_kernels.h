@@ -19,7 +19,16 @@ struct TraceArgs {
   uint64_t total_units; // pixels * s_count  (< 2^32)
   uint64_t seedmix;     // splitmix64(seed)
   unsigned long long* work_counter;
-  unsigned long long* ray_counter;
+  unsigned long long* ray_counter;  // [0] rays, [1] sphere tests, [2] box tests
+};
+
+struct BvhView {
+  const float4* __restrict__ nodes;      // 2 x float4 per node: {lo, skip}, {hi, leaf}
+  const double4* __restrict__ leaf_geo;  // sphere per leaf slot
+  const int* __restrict__ leaf_idx;      // original index per leaf slot
+  const int* __restrict__ big_idx;       // spheres tested on every ray
+  int n_nodes, n_big;
+  double r_check;
 };
 
 struct ReduceArgs {
@@ -32,14 +41,15 @@ struct ReduceArgs {
   unsigned char* rgb8;    // [pixels][3] or nullptr (last chunk only)
 };
 
+template <bool kBVH>
 __global__ void psrt_trace(const double4* __restrict__ geo, const double* __restrict__ inv_r,
-                           double* __restrict__ samples, TraceArgs a);
+                           double* __restrict__ samples, TraceArgs a, BvhView bv);
 __global__ void psrt_reduce(ReduceArgs a);
 __global__ void psrt_quantize(const double* __restrict__ accum, unsigned char* __restrict__ rgb8,
                               unsigned n, int spp);
 __global__ void psrt_probe_hit(const double4* __restrict__ geo, const double* __restrict__ inv_r,
                                int n, const double* __restrict__ rays, double* __restrict__ out,
-                               unsigned count);
+                               unsigned count, BvhView bv, int use_bvh);
 __global__ void psrt_probe_f64(int op, const double* __restrict__ x, const double* __restrict__ y,
                                double* __restrict__ out, unsigned n);
 

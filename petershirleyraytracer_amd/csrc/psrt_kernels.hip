@@ -100,10 +100,117 @@ __device__ __forceinline__ HitRec hit_record_of(const double4 s, double ir, doub
   return h;
 }
 
+// ---- exact culling ------------------------------------------
+//
+// The reference's list scan returns the lexicographic minimum of (tau_j, -j)
+// over spheres with a root tau_j in [0, closest] (tau_j: near root if >= 0,
+// else far root if >= 0 — independent of closest, sphere.cc:24-31). So any
+// visiting order that evaluates every sphere whose root could land in
+// [0, closest], with the same FP64 test, returns the same record. The BVH
+// (psrt_bvh.h) visits a superset: its FP32 boxes are padded past the FP32
+// slab error and the FP64 root error; rays it cannot bound (non-finite,
+// |o| > r_check, A not in (0, 1e200)) take the linear sweep.
+
+// sphere.cc:6-31 for one sphere, then the (t, index) rule of the list scan.
+__device__ __forceinline__ void test_sphere(const double4 s, int idx, double ox, double oy,
+                                            double oz, double dx, double dy, double dz,
+                                            double A, double& best_t, int& best_i) {
+  const double ax = ox - s.x, ay = oy - s.y, az = oz - s.z;
+  const double hb = (dx * ax + dy * ay) + dz * az;
+  const double c = ((ax * ax + ay * ay) + az * az) - s.w;
+  const double disc = hb * hb - A * c;
+  if (disc < 0.0) return;
+  const double sq = __builtin_sqrt(disc);
+  double t = (-hb - sq) / A;
+  if (t < 0.0 || t > best_t) {
+    t = (-hb + sq) / A;
+    if (t < 0.0 || t > best_t) return;
+  }
+  if (t < best_t || idx > best_i) {  // equal t: the later index wins
+    best_t = t;
+    best_i = idx;
+  }
+}
+
+
+__device__ __forceinline__ float tmax_up(double t) {
+  // >= t for every finite t (float rounding <= 2^-24 relative; margin 2^-21)
+  return (float)t * 1.00000048f;
+}
+
+__device__ __forceinline__ float safe_inv(float d) {
+  const float m = __builtin_fabsf(d) < 1e-20f ? __builtin_copysignf(1e-20f, d) : d;
+  return 1.0f / m;
+}
+
+struct CullStats {
+  unsigned boxes, spheres;
+};
+
+__device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, int n,
+                                             const BvhView& bv, int hint, double ox, double oy,
+                                             double oz, double dx, double dy, double dz, double A,
+                                             double& best_t, CullStats& cs) {
+  const bool bounded = (A > 0.0) && (A < 1e200) && __builtin_fabs(ox) <= bv.r_check &&
+                       __builtin_fabs(oy) <= bv.r_check && __builtin_fabs(oz) <= bv.r_check;
+  if (!bounded) {
+    cs.spheres += n;
+    return sweep_linear(geo, n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), best_t);
+  }
+  double bt = __builtin_inf();
+  int bi = -1;
+  if (hint >= 0) {
+    test_sphere(geo[hint], hint, ox, oy, oz, dx, dy, dz, A, bt, bi);
+    ++cs.spheres;
+  }
+  for (int b = 0; b < bv.n_big; ++b) {
+    const int idx = bv.big_idx[b];
+    if (idx != hint) test_sphere(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
+  }
+  cs.spheres += bv.n_big;
+  const float fox = (float)ox, foy = (float)oy, foz = (float)oz;
+  const float ix = safe_inv((float)dx), iy = safe_inv((float)dy), iz = safe_inv((float)dz);
+  const float oix = fox * ix, oiy = foy * iy, oiz = foz * iz;
+  float tmax = tmax_up(bt);
+  int node = 0;
+  while (node < bv.n_nodes) {
+    const float4 a = bv.nodes[2 * node];
+    const float4 b = bv.nodes[2 * node + 1];
+    // slab distances; FP32 FMA is fine here: the test only needs to be
+    // conservative, and the box padding covers its rounding (psrt_bvh.cpp)
+    const float x0 = __builtin_fmaf(a.x, ix, -oix), x1 = __builtin_fmaf(b.x, ix, -oix);
+    const float y0 = __builtin_fmaf(a.y, iy, -oiy), y1 = __builtin_fmaf(b.y, iy, -oiy);
+    const float z0 = __builtin_fmaf(a.z, iz, -oiz), z1 = __builtin_fmaf(b.z, iz, -oiz);
+    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.0f));
+    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tmax));
+    ++cs.boxes;
+    const int skip = __float_as_int(a.w);
+    const int leaf = __float_as_int(b.w);
+    if (tn <= tf) {
+      if (leaf < 0) {
+        ++node;
+        continue;
+      }
+      const int first = leaf >> 8, cnt = leaf & 255;
+      for (int k = first; k < first + cnt; ++k) {
+        const int idx = bv.leaf_idx[k];
+        if (idx == hint) continue;
+        test_sphere(bv.leaf_geo[k], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
+        ++cs.spheres;
+      }
+      tmax = tmax_up(bt);
+    }
+    node = skip;
+  }
+  best_t = bt;
+  return bi;
+}
+
+template <bool kBVH>
 __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restrict__ geo,
                                                           const double* __restrict__ inv_r,
                                                           double* __restrict__ samples,
-                                                          TraceArgs a) {
+                                                          TraceArgs a, BvhView bv) {
   const unsigned lane = lane_id();
   const uint64_t total = a.total_units;
 
@@ -119,6 +226,8 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
   unsigned q = 0;     // pixel index within the shard
   unsigned sl = 0;    // sample index within the chunk
   unsigned rays = 0;
+  int hint = -1;  // sphere the ray starts on (the previous hit), tested first
+  CullStats cs{0u, 0u};
 
   for (;;) {
     // ---- refill lanes whose sample finished (wavefront ballot compaction) ----
@@ -153,6 +262,7 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
           dz = ((a.llc[2] + u * a.hor[2]) + v * a.ver[2]) - oz;
           A = (dx * dx + dy * dy) + dz * dz;
           k = 0;
+          hint = -1;
           active = true;
         }
       }
@@ -176,8 +286,13 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
       } else {
         ++rays;
         double t;
-        const int hit =
-            sweep_linear(geo, a.n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), t);
+        int hit;
+        if constexpr (kBVH) {
+          hit = world_hit_bvh(geo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, t, cs);
+        } else {
+          hit = sweep_linear(geo, a.n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), t);
+          cs.spheres += a.n;
+        }
         if (hit >= 0) {
           if (k >= a.max_depth) {  // depth 0 hit: 0.5 * ray_color(.., -1) = black
             col_r = col_g = col_b = 0.0;
@@ -200,6 +315,7 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
             dz = ((pz + nz) + rz) - pz;
             ox = px, oy = py, oz = pz;
             A = (dx * dx + dy * dy) + dz * dz;
+            hint = hit;
             ++k;
           }
         } else {
@@ -223,11 +339,24 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
     }
   }
 
-  // rays traced by this wave -> one atomic
-  unsigned long long wr = rays;
-  for (int off = 32; off > 0; off >>= 1) wr += __shfl_xor(wr, off);
-  if (lane == 0 && wr) atomicAdd(a.ray_counter, wr);
+  // rays / sphere tests / box tests of this wave -> one atomic each
+  unsigned long long wr = rays, ws = cs.spheres, wb = cs.boxes;
+  for (int off = 32; off > 0; off >>= 1) {
+    wr += __shfl_xor(wr, off);
+    ws += __shfl_xor(ws, off);
+    wb += __shfl_xor(wb, off);
+  }
+  if (lane == 0) {
+    if (wr) atomicAdd(a.ray_counter, wr);
+    if (ws) atomicAdd(a.ray_counter + 1, ws);
+    if (wb) atomicAdd(a.ray_counter + 2, wb);
+  }
 }
+
+template __global__ void psrt_trace<false>(const double4* __restrict__, const double* __restrict__,
+                                           double* __restrict__, TraceArgs, BvhView);
+template __global__ void psrt_trace<true>(const double4* __restrict__, const double* __restrict__,
+                                          double* __restrict__, TraceArgs, BvhView);
 
 // pixel_color += sample, in sample order (main.cc:77-84); write_color on the
 // last chunk (color.h:8-24).
@@ -281,14 +410,20 @@ __global__ __launch_bounds__(256) void psrt_quantize(const double* __restrict__ 
 // out[k] = {index, px, py, pz, nx, ny, nz, t, front_face}.
 __global__ void psrt_probe_hit(const double4* __restrict__ geo, const double* __restrict__ inv_r,
                                int n, const double* __restrict__ rays, double* __restrict__ out,
-                               unsigned count) {
+                               unsigned count, BvhView bv, int use_bvh) {
   const unsigned k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= count) return;
   const double* r = rays + (size_t)k * 8;
   const double ox = r[0], oy = r[1], oz = r[2], dx = r[3], dy = r[4], dz = r[5];
   const double A = (dx * dx + dy * dy) + dz * dz;  // sphere.cc:9
   double t;
-  const int i = sweep_linear(geo, n, ox, oy, oz, dx, dy, dz, A, r[6], r[7], t);
+  int i;
+  if (use_bvh && r[6] == 0.0 && r[7] == __builtin_inf()) {  // the trace kernel's call shape
+    CullStats cs{0u, 0u};
+    i = world_hit_bvh(geo, n, bv, -1, ox, oy, oz, dx, dy, dz, A, t, cs);
+  } else {
+    i = sweep_linear(geo, n, ox, oy, oz, dx, dy, dz, A, r[6], r[7], t);
+  }
   double* o = out + (size_t)k * 9;
   o[0] = (double)i;
   if (i >= 0) {

@@ -45,9 +45,12 @@ def _camera_array(c: RtCamera) -> np.ndarray:
                      list(c.vertical)], dtype=np.float64)
 
 
+FLAG_NO_CULL = 1
+
+
 def params(width: int, height: int, spp: int, max_depth: int = 50, seed: int = 0,
-           row_offset: int = 0, row_stride: int = 1) -> RtParams:
-    return RtParams(width, height, spp, max_depth, seed, row_offset, row_stride, 0)
+           row_offset: int = 0, row_stride: int = 1, flags: int = 0) -> RtParams:
+    return RtParams(width, height, spp, max_depth, seed, row_offset, row_stride, flags)
 
 
 def rows_owned(height: int, row_offset: int = 0, row_stride: int = 1) -> int:
@@ -85,11 +88,13 @@ def scene_random_spheres(seed: int = 1) -> np.ndarray:
 
 def stats_dict(s: RtStats) -> dict:
     return dict(samples=s.samples, rays=s.rays, sphere_tests=s.sphere_tests,
+                tests_executed=s.tests_executed, box_tests=s.box_tests,
                 kernel_ms=s.kernel_ms, total_ms=s.total_ms)
 
 
 def render(spheres, camera, width: int, height: int, spp: int, max_depth: int = 50,
-           seed: int = 0, row_offset: int = 0, row_stride: int = 1, want_rgb: bool = True):
+           seed: int = 0, row_offset: int = 0, row_stride: int = 1, want_rgb: bool = True,
+           cull: bool = True):
     """One-shot render of the owned rows on the default device (RT_DEVICE).
 
     Returns (accum[rows, W, 3] float64, rgb8[rows, W, 3] uint8 or None, stats dict).
@@ -97,7 +102,8 @@ def render(spheres, camera, width: int, height: int, spp: int, max_depth: int = 
     L = _lib.load()
     sp, n = _spheres(spheres)
     cam = _camera(camera)
-    p = params(width, height, spp, max_depth, seed, row_offset, row_stride)
+    p = params(width, height, spp, max_depth, seed, row_offset, row_stride,
+               0 if cull else FLAG_NO_CULL)
     rows = L.rt_rows_owned(height, row_offset, row_stride)
     if rows <= 0:
         raise _lib.RtError(f"shard owns no rows: height={height} offset={row_offset} "
@@ -201,13 +207,15 @@ def probe_f64(op: int, x: np.ndarray, y: Optional[np.ndarray] = None) -> np.ndar
     return out
 
 
-def world_hit(spheres, rays: np.ndarray) -> np.ndarray:
+def world_hit(spheres, rays: np.ndarray, cull: bool = True) -> np.ndarray:
     """hittable_list::hit on the device for rays[k] = (o, d, tmin, tmax);
-    returns out[k] = (index, p, normal, t, front_face) (debug / KAT entry)."""
+    returns out[k] = (index, p, normal, t, front_face) (debug / KAT entry).
+    With cull, rays with tmin == 0, tmax == inf go through the BVH path."""
     sp, n = _spheres(spheres)
     r = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 8)
     out = np.zeros((len(r), 9), dtype=np.float64)
     P = C.POINTER(C.c_double)
     check(_lib.load().rt_debug_world_hit(sp, n, r.ctypes.data_as(P), len(r),
-                                         out.ctypes.data_as(P)), "rt_debug_world_hit")
+                                         out.ctypes.data_as(P), 1 if cull else 0),
+          "rt_debug_world_hit")
     return out
