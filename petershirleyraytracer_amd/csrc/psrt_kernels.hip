@@ -151,9 +151,10 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
                                              const BvhView& bv, int hint, double ox, double oy,
                                              double oz, double dx, double dy, double dz, double A,
                                              double& best_t, CullStats& cs) {
-  const bool bounded = (A > 0.0) && (A < 1e200) && __builtin_fabs(ox) <= bv.r_check &&
-                       __builtin_fabs(oy) <= bv.r_check && __builtin_fabs(oz) <= bv.r_check;
-  if (!bounded) {
+  const bool finite = (A > 0.0) && (A < 1e200);
+  const double am = __builtin_fmax(__builtin_fabs(ox),
+                                   __builtin_fmax(__builtin_fabs(oy), __builtin_fabs(oz)));
+  if (!finite || !(am < 1e200)) {
     cs.spheres += n;
     return sweep_linear(geo, n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), best_t);
   }
@@ -168,6 +169,34 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
     if (idx != hint) test_sphere(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
   }
   cs.spheres += bv.n_big;
+  if (!(am <= bv.r_check)) {
+    // Far origin (e.g. inside the r=1000 ground): the FP32 slab bound does not
+    // hold. Test [0, bt] against the padded root box in FP64 (error ~1e-13
+    // relative, far inside the pad): a miss proves no BVH sphere can have a
+    // root in [0, bt]; a hit takes the exact linear sweep.
+    const float4 ra = bv.nodes[0], rb = bv.nodes[1];
+    double t0 = 0.0, t1 = bt;
+    const double o3[3] = {ox, oy, oz}, d3[3] = {dx, dy, dz};
+    const double lo3[3] = {ra.x, ra.y, ra.z}, hi3[3] = {rb.x, rb.y, rb.z};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (d3[k] == 0.0) {
+        if (o3[k] < lo3[k] || o3[k] > hi3[k]) t0 = 2.0, t1 = 1.0;  // parallel, outside
+      } else {
+        const double inv = 1.0 / d3[k];
+        const double u = (lo3[k] - o3[k]) * inv, v = (hi3[k] - o3[k]) * inv;
+        t0 = __builtin_fmax(t0, __builtin_fmin(u, v));
+        t1 = __builtin_fmin(t1, __builtin_fmax(u, v));
+      }
+    }
+    ++cs.boxes;
+    if (t0 <= t1 * (1.0 + 0x1p-40) + 0x1p-40) {
+      cs.spheres += n;
+      return sweep_linear(geo, n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), best_t);
+    }
+    best_t = bt;
+    return bi;
+  }
   const float fox = (float)ox, foy = (float)oy, foz = (float)oz;
   const float ix = safe_inv((float)dx), iy = safe_inv((float)dy), iz = safe_inv((float)dz);
   const float oix = fox * ix, oiy = foy * iy, oiz = foz * iz;
