@@ -154,14 +154,14 @@ int rt_context_create(int device, rt_context** out) {
   HIP_TRY(hipGetDeviceProperties(&prop, device));
   c->cus = prop.multiProcessorCount;
   int per_cu = 0;
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace<false>,
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace<false, false>,
                                                         psrt::kTraceBlock, 0));
   c->grid = c->cus * (per_cu < 1 ? 1 : per_cu);
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace<true>,
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace<true, false>,
                                                         psrt::kTraceBlock, 0));
   c->grid_bvh = c->cus * (per_cu < 1 ? 1 : per_cu);
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  HIP_TRY(hipMalloc(&c->d_counters, 4 * sizeof(unsigned long long)));
+  HIP_TRY(hipMalloc(&c->d_counters, 16 * sizeof(unsigned long long)));
   HIP_TRY(hipEventCreate(&c->ev_all0));
   HIP_TRY(hipEventCreate(&c->ev_all1));
   *out = c;
@@ -327,7 +327,9 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   ta.work_counter = c->d_counters;
   ta.ray_counter = c->d_counters + 1;
 
-  HIP_TRY(hipMemsetAsync(c->d_counters + 1, 0, 3 * sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(c->d_counters + 1, 0, 15 * sizeof(unsigned long long), st));
+  const bool stamps = std::getenv("PSRT_STAMPS") != nullptr;  // diagnostic build
+  ta.stamps = c->d_counters + 8;
   const bool use_bvh = c->bvh && !(p->flags & RT_FLAG_NO_CULL);
   const psrt::BvhView bv = bvh_view(c);
   HIP_TRY(hipEventRecord(c->ev_all0, st));
@@ -339,14 +341,21 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     ta.total_units = (uint64_t)P * sc;
     HIP_TRY(hipMemsetAsync(c->d_counters, 0, sizeof(unsigned long long), st));
     HIP_TRY(hipEventRecord(c->ev[2 * ch], st));
-    if (use_bvh)
-      hipLaunchKernelGGL(psrt::psrt_trace<true>, dim3(c->grid_bvh), dim3(psrt::kTraceBlock), 0,
-                         st, (const double4*)c->d_geo, (const double*)c->d_inv_r, c->d_samples,
-                         ta, bv);
+    const double4* g4 = c->d_geo;
+    const double* ir = c->d_inv_r;
+    const dim3 blk(psrt::kTraceBlock);
+    if (use_bvh && !stamps)
+      hipLaunchKernelGGL((psrt::psrt_trace<true, false>), dim3(c->grid_bvh), blk, 0, st, g4, ir,
+                         c->d_samples, ta, bv);
+    else if (use_bvh)
+      hipLaunchKernelGGL((psrt::psrt_trace<true, true>), dim3(c->grid_bvh), blk, 0, st, g4, ir,
+                         c->d_samples, ta, bv);
+    else if (!stamps)
+      hipLaunchKernelGGL((psrt::psrt_trace<false, false>), dim3(c->grid), blk, 0, st, g4, ir,
+                         c->d_samples, ta, bv);
     else
-      hipLaunchKernelGGL(psrt::psrt_trace<false>, dim3(c->grid), dim3(psrt::kTraceBlock), 0, st,
-                         (const double4*)c->d_geo, (const double*)c->d_inv_r, c->d_samples, ta,
-                         bv);
+      hipLaunchKernelGGL((psrt::psrt_trace<false, true>), dim3(c->grid), blk, 0, st, g4, ir,
+                         c->d_samples, ta, bv);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[2 * ch + 1], st));
     psrt::ReduceArgs ra{};
@@ -388,6 +397,16 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   c->last.sphere_tests = rays * (uint64_t)(c->n_last > 0 ? c->n_last : 0);
   c->last.tests_executed = cnt[1];
   c->last.box_tests = cnt[2];
+  if (std::getenv("PSRT_STAMPS")) {
+    unsigned long long sec[5];
+    HIP_TRY(hipMemcpy(sec, c->d_counters + 8, sizeof sec, hipMemcpyDeviceToHost));
+    double tot = 0;
+    for (auto v : sec) tot += (double)v;
+    std::fprintf(stderr,
+                 "{\"psrt_sections\": {\"refill\": %.4f, \"hit\": %.4f, \"scatter\": %.4f, "
+                 "\"shade\": %.4f, \"other\": %.4f, \"wave_cycles\": %.4g}}\n",
+                 sec[0] / tot, sec[1] / tot, sec[2] / tot, sec[3] / tot, sec[4] / tot, tot);
+  }
   c->last.kernel_ms = kms;
   c->last.total_ms = all;
   if (s) *s = c->last;

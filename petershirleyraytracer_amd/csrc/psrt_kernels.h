@@ -20,6 +20,7 @@ struct TraceArgs {
   uint64_t seedmix;     // splitmix64(seed)
   unsigned long long* work_counter;
   unsigned long long* ray_counter;  // [0] rays, [1] sphere tests, [2] box tests
+  unsigned long long* stamps;       // diagnostic build: cycles per section (kSecCount)
 };
 
 struct BvhView {
@@ -41,7 +42,7 @@ struct ReduceArgs {
   unsigned char* rgb8;    // [pixels][3] or nullptr (last chunk only)
 };
 
-template <bool kBVH>
+template <bool kBVH, bool kStamps>
 __global__ void psrt_trace(const double4* __restrict__ geo, const double* __restrict__ inv_r,
                            double* __restrict__ samples, TraceArgs a, BvhView bv);
 __global__ void psrt_reduce(ReduceArgs a);

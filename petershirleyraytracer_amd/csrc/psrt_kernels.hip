@@ -28,6 +28,33 @@ namespace psrt {
 
 __device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
 
+// Diagnostic build only (kStamps): wave-level cycle accounting per kernel
+// section, one s_memtime per boundary (cdna_hip_programming.md §7 stamps).
+// Read its SHARES, never its run time.
+enum Section { kSecRefill = 0, kSecHit, kSecScatter, kSecShade, kSecOther, kSecCount };
+
+template <bool kOn>
+struct SectionClock {
+  uint64_t t = 0, acc[kSecCount] = {0, 0, 0, 0, 0};
+  __device__ __forceinline__ void start() {
+    if constexpr (kOn) t = now();
+  }
+  __device__ __forceinline__ void mark(int sec) {
+    if constexpr (kOn) {
+      const uint64_t n = now();
+      acc[sec] += n - t;
+      t = n;
+    }
+  }
+  static __device__ __forceinline__ uint64_t now() {
+    uint64_t v;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return v;
+  }
+};
+
 __device__ __forceinline__ unsigned mbcnt64(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                    __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
@@ -235,7 +262,7 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
   return bi;
 }
 
-template <bool kBVH>
+template <bool kBVH, bool kStamps>
 __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restrict__ geo,
                                                           const double* __restrict__ inv_r,
                                                           double* __restrict__ samples,
@@ -257,6 +284,8 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
   unsigned rays = 0;
   int hint = -1;  // sphere the ray starts on (the previous hit), tested first
   CullStats cs{0u, 0u};
+  SectionClock<kStamps> clk;
+  clk.start();
 
   for (;;) {
     // ---- refill lanes whose sample finished (wavefront ballot compaction) ----
@@ -304,68 +333,73 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
       }
       if (win_base >= total) exhausted = true;
     }
+    clk.mark(kSecRefill);
     if (__ballot(active) == 0) break;
 
+    // ---- world.hit(r, 0, inf, rec)  (main.cc:40) ----
+    int hit = -1;
+    double t = 0.0;
+    bool finish = false;
+    double col_r = 0.0, col_g = 0.0, col_b = 0.0;
     if (active) {
-      double col_r, col_g, col_b;
-      bool finish = false;
-      if (a.max_depth < 0) {  // main.cc:36-37 at the first call
-        col_r = col_g = col_b = 0.0;
+      if (a.max_depth < 0) {  // main.cc:36-37 at the first call: black, no trace
         finish = true;
       } else {
         ++rays;
-        double t;
-        int hit;
         if constexpr (kBVH) {
           hit = world_hit_bvh(geo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, t, cs);
         } else {
           hit = sweep_linear(geo, a.n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), t);
           cs.spheres += a.n;
         }
-        if (hit >= 0) {
-          if (k >= a.max_depth) {  // depth 0 hit: 0.5 * ray_color(.., -1) = black
-            col_r = col_g = col_b = 0.0;
-            finish = true;
-          } else {
-            const HitRec h = hit_record_of(geo[hit], inv_r[hit], t, ox, oy, oz, dx, dy, dz);
-            const double px = h.px, py = h.py, pz = h.pz;
-            const double nx = h.nx, ny = h.ny, nz = h.nz;
-            // vec3.h:83-95 (g++ order: z, y, x) and vec3.h:102-109
-            double rx, ry, rz;
-            do {
-              rz = random_pm1(rng);
-              ry = random_pm1(rng);
-              rx = random_pm1(rng);
-            } while ((rx * rx + ry * ry) + rz * rz > 1.0);
-            if (!((rx * nx + ry * ny) + rz * nz > 0.0)) rx = -rx, ry = -ry, rz = -rz;
-            // main.cc:42-43: target = (p + n) + rv; ray(p, target - p)
-            dx = ((px + nx) + rx) - px;
-            dy = ((py + ny) + ry) - py;
-            dz = ((pz + nz) + rz) - pz;
-            ox = px, oy = py, oz = pz;
-            A = (dx * dx + dy * dy) + dz * dz;
-            hint = hit;
-            ++k;
-          }
-        } else {
-          // main.cc:46-48, times 0.5^k (main.cc:43 unwound; exact)
-          const double y = (1.0 / __builtin_sqrt(A)) * dy;
-          const double tt = 0.5 * (y + 1.0);
-          const double w = 1.0 - tt;
-          col_r = half_pow(w + tt * 0.5, k);
-          col_g = half_pow(w + tt * 0.7, k);
-          col_b = half_pow(w + tt * 1.0, k);
-          finish = true;
-        }
-      }
-      if (finish) {
-        double* dst = samples + ((size_t)sl * a.pixels + q) * 3;
-        dst[0] = col_r;
-        dst[1] = col_g;
-        dst[2] = col_b;
-        active = false;
+        // depth-0 hit: 0.5 * ray_color(.., -1) = black (main.cc:36-37, 43)
+        if (hit < 0 || k >= a.max_depth) finish = true;
       }
     }
+    clk.mark(kSecHit);
+
+    // ---- scatter: target = (p + n) + random_in_hemisphere(n)  (main.cc:42-43) ----
+    if (active && !finish) {
+      const HitRec h = hit_record_of(geo[hit], inv_r[hit], t, ox, oy, oz, dx, dy, dz);
+      // vec3.h:83-95 (g++ order: z, y, x) and vec3.h:102-109
+      double rx, ry, rz;
+      do {
+        rz = random_pm1(rng);
+        ry = random_pm1(rng);
+        rx = random_pm1(rng);
+      } while ((rx * rx + ry * ry) + rz * rz > 1.0);
+      if (!((rx * h.nx + ry * h.ny) + rz * h.nz > 0.0)) rx = -rx, ry = -ry, rz = -rz;
+      dx = ((h.px + h.nx) + rx) - h.px;
+      dy = ((h.py + h.ny) + ry) - h.py;
+      dz = ((h.pz + h.nz) + rz) - h.pz;
+      ox = h.px, oy = h.py, oz = h.pz;
+      A = (dx * dx + dy * dy) + dz * dz;
+      hint = hit;
+      ++k;
+    }
+    clk.mark(kSecScatter);
+
+    // ---- sample done: sky (main.cc:46-48) x 0.5^k, or black; store ----
+    if (active && finish) {
+      if (hit < 0 && a.max_depth >= 0) {
+        const double y = (1.0 / __builtin_sqrt(A)) * dy;
+        const double tt = 0.5 * (y + 1.0);
+        const double w = 1.0 - tt;
+        col_r = half_pow(w + tt * 0.5, k);
+        col_g = half_pow(w + tt * 0.7, k);
+        col_b = half_pow(w + tt * 1.0, k);
+      }
+      double* dst = samples + ((size_t)sl * a.pixels + q) * 3;
+      dst[0] = col_r;
+      dst[1] = col_g;
+      dst[2] = col_b;
+      active = false;
+    }
+    clk.mark(kSecShade);
+  }
+  if constexpr (kStamps) {
+    if (lane == 0)
+      for (int k2 = 0; k2 < kSecCount; ++k2) atomicAdd(a.stamps + k2, (unsigned long long)clk.acc[k2]);
   }
 
   // rays / sphere tests / box tests of this wave -> one atomic each
@@ -382,10 +416,14 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
   }
 }
 
-template __global__ void psrt_trace<false>(const double4* __restrict__, const double* __restrict__,
-                                           double* __restrict__, TraceArgs, BvhView);
-template __global__ void psrt_trace<true>(const double4* __restrict__, const double* __restrict__,
-                                          double* __restrict__, TraceArgs, BvhView);
+#define PSRT_INSTANTIATE(B, S)                                                             \
+  template __global__ void psrt_trace<B, S>(const double4* __restrict__, const double* __restrict__, \
+                                            double* __restrict__, TraceArgs, BvhView);
+PSRT_INSTANTIATE(false, false)
+PSRT_INSTANTIATE(true, false)
+PSRT_INSTANTIATE(false, true)
+PSRT_INSTANTIATE(true, true)
+#undef PSRT_INSTANTIATE
 
 // pixel_color += sample, in sample order (main.cc:77-84); write_color on the
 // last chunk (color.h:8-24).
