@@ -181,6 +181,40 @@ BvhHost build_bvh(const rt_sphere* s, int n) {
   }
   Builder bld{prims, out};
   bld.build(0, (int)prims.size(), 0);
+
+  // point-location grid: cells ~2.5 median radii wide, at most 128 per axis
+  Box all;
+  for (const Prim& p : prims) all.grow(p.box);
+  double ext = 0.0;
+  for (int k = 0; k < 3; ++k) ext = std::max(ext, all.hi[k] - all.lo[k]);
+  double cell = std::max(2.5 * median, ext / 128.0);
+  if (!(cell > 0)) cell = std::max(ext, 1.0);
+  GridHost& g = out.grid;
+  g.cell = cell;
+  long ncell = 1;
+  for (int k = 0; k < 3; ++k) {
+    g.lo[k] = all.lo[k];
+    g.dims[k] = std::max(1, (int)std::ceil((all.hi[k] - all.lo[k]) / cell));
+    ncell *= g.dims[k];
+  }
+  std::vector<std::vector<int32_t>> cells((size_t)ncell);
+  auto cidx = [&](int x, int y, int z) { return ((long)z * g.dims[1] + y) * g.dims[0] + x; };
+  for (const Prim& p : prims) {
+    int c0[3], c1[3];
+    for (int k = 0; k < 3; ++k) {
+      c0[k] = std::max(0, std::min(g.dims[k] - 1, (int)std::floor((p.box.lo[k] - g.lo[k]) / cell)));
+      c1[k] = std::max(0, std::min(g.dims[k] - 1, (int)std::floor((p.box.hi[k] - g.lo[k]) / cell)));
+    }
+    for (int z = c0[2]; z <= c1[2]; ++z)
+      for (int y = c0[1]; y <= c1[1]; ++y)
+        for (int x = c0[0]; x <= c1[0]; ++x) cells[cidx(x, y, z)].push_back(p.idx);
+  }
+  g.start.resize(ncell + 1);
+  g.start[0] = 0;
+  for (long c = 0; c < ncell; ++c) {
+    g.start[c + 1] = g.start[c] + (int32_t)cells[c].size();
+    g.items.insert(g.items.end(), cells[c].begin(), cells[c].end());
+  }
   out.enabled = true;
   return out;
 }

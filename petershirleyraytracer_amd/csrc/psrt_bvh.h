@@ -33,7 +33,20 @@ constexpr int kBvhMinSpheres = 17;   // below this the linear sweep wins
 constexpr double kBigRatio = 16.0;   // radius > 16 x median -> tested every ray
 constexpr int kLeafMax = 2;
 
+// Point-location grid over the same padded boxes: cell -> spheres whose padded
+// box overlaps the cell. A ray whose segment [o, o + closest*d] lies inside one
+// cell can only hit those spheres (its hit point is inside the hit sphere's
+// padded box and inside the cell).
+struct GridHost {
+  double lo[3] = {0, 0, 0};
+  double cell = 1.0;
+  int dims[3] = {0, 0, 0};
+  std::vector<int32_t> start;  // dims[0]*dims[1]*dims[2] + 1 offsets into items
+  std::vector<int32_t> items;  // original sphere indices
+};
+
 struct BvhHost {
+  GridHost grid;
   std::vector<BvhNode> nodes;
   std::vector<int32_t> leaf_idx;  // original sphere index per leaf slot
   std::vector<int32_t> big_idx;   // original indices tested on every ray

@@ -68,6 +68,10 @@ struct rt_context {
   double4* d_leaf_geo = nullptr;
   int* d_leaf_idx = nullptr;
   int* d_big = nullptr;
+  int* d_cell_start = nullptr;
+  int* d_cell_items = nullptr;
+  psrt::GridHost pgrid;  // point-location grid (host copy of the geometry)
+  double pad = 0.0;
   int n_nodes = 0, n_big = 0, n_leaf = 0;
   double r_check = 0.0;
   hipStream_t stream = nullptr;
@@ -161,7 +165,7 @@ int rt_context_create(int device, rt_context** out) {
                                                         psrt::kTraceBlock, 0));
   c->grid_bvh = c->cus * (per_cu < 1 ? 1 : per_cu);
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  HIP_TRY(hipMalloc(&c->d_counters, 16 * sizeof(unsigned long long)));
+  HIP_TRY(hipMalloc(&c->d_counters, 32 * sizeof(unsigned long long)));
   HIP_TRY(hipEventCreate(&c->ev_all0));
   HIP_TRY(hipEventCreate(&c->ev_all1));
   *out = c;
@@ -181,6 +185,8 @@ int rt_context_destroy(rt_context* c) {
   (void)hipFree(c->d_leaf_geo);
   (void)hipFree(c->d_leaf_idx);
   (void)hipFree(c->d_big);
+  (void)hipFree(c->d_cell_start);
+  (void)hipFree(c->d_cell_items);
   for (auto e : c->ev) (void)hipEventDestroy(e);
   if (c->ev_all0) (void)hipEventDestroy(c->ev_all0);
   if (c->ev_all1) (void)hipEventDestroy(c->ev_all1);
@@ -225,7 +231,10 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
   (void)hipFree(c->d_leaf_geo);
   (void)hipFree(c->d_leaf_idx);
   (void)hipFree(c->d_big);
+  (void)hipFree(c->d_cell_start);
+  (void)hipFree(c->d_cell_items);
   c->d_nodes = nullptr, c->d_leaf_geo = nullptr, c->d_leaf_idx = nullptr, c->d_big = nullptr;
+  c->d_cell_start = nullptr, c->d_cell_items = nullptr;
   c->bvh = b.enabled;
   c->n_nodes = c->n_big = c->n_leaf = 0;
   if (b.enabled) {
@@ -248,6 +257,16 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
     if (c->n_big > 0)
       HIP_TRY(hipMemcpy(c->d_big, b.big_idx.data(), b.big_idx.size() * sizeof(int),
                         hipMemcpyHostToDevice));
+    c->pgrid = b.grid;
+    c->pad = b.pad;
+    const size_t ns = b.grid.start.size(), ni = std::max<size_t>(1, b.grid.items.size());
+    HIP_TRY(hipMalloc(&c->d_cell_start, ns * sizeof(int)));
+    HIP_TRY(hipMalloc(&c->d_cell_items, ni * sizeof(int)));
+    HIP_TRY(hipMemcpy(c->d_cell_start, b.grid.start.data(), ns * sizeof(int),
+                      hipMemcpyHostToDevice));
+    if (!b.grid.items.empty())
+      HIP_TRY(hipMemcpy(c->d_cell_items, b.grid.items.data(), b.grid.items.size() * sizeof(int),
+                        hipMemcpyHostToDevice));
   }
   return RT_OK;
 }
@@ -261,6 +280,15 @@ static psrt::BvhView bvh_view(const rt_context* c) {
   v.n_nodes = c->n_nodes;
   v.n_big = c->n_big;
   v.r_check = c->r_check;
+  v.cell_start = c->d_cell_start;
+  v.cell_items = c->d_cell_items;
+  for (int k = 0; k < 3; ++k) {
+    v.glo[k] = c->pgrid.lo[k];
+    v.gdims[k] = c->pgrid.dims[k];
+  }
+  v.gcell = c->pgrid.cell;
+  v.ginv = 1.0 / c->pgrid.cell;
+  v.gmargin = c->pad * 0.25;
   return v;
 }
 
@@ -327,7 +355,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   ta.work_counter = c->d_counters;
   ta.ray_counter = c->d_counters + 1;
 
-  HIP_TRY(hipMemsetAsync(c->d_counters + 1, 0, 15 * sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(c->d_counters + 1, 0, 31 * sizeof(unsigned long long), st));
   const bool stamps = std::getenv("PSRT_STAMPS") != nullptr;  // diagnostic build
   ta.stamps = c->d_counters + 8;
   const bool use_bvh = c->bvh && !(p->flags & RT_FLAG_NO_CULL);
@@ -398,14 +426,17 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   c->last.tests_executed = cnt[1];
   c->last.box_tests = cnt[2];
   if (std::getenv("PSRT_STAMPS")) {
-    unsigned long long sec[5];
+    unsigned long long sec[9];
     HIP_TRY(hipMemcpy(sec, c->d_counters + 8, sizeof sec, hipMemcpyDeviceToHost));
     double tot = 0;
-    for (auto v : sec) tot += (double)v;
+    for (int k = 0; k < 5; ++k) tot += (double)sec[k];
     std::fprintf(stderr,
                  "{\"psrt_sections\": {\"refill\": %.4f, \"hit\": %.4f, \"scatter\": %.4f, "
-                 "\"shade\": %.4f, \"other\": %.4f, \"wave_cycles\": %.4g}}\n",
-                 sec[0] / tot, sec[1] / tot, sec[2] / tot, sec[3] / tot, sec[4] / tot, tot);
+                 "\"shade\": %.4f, \"other\": %.4f, \"wave_cycles\": %.4g, "
+                 "\"wave_trips\": %llu, \"wave_leaf_trips\": %llu, \"trav_rays\": %llu, "
+                 "\"lane_boxes\": %llu, \"leaf_visits\": %llu, \"rays\": %llu}}\n",
+                 sec[0] / tot, sec[1] / tot, sec[2] / tot, sec[3] / tot, sec[4] / tot, tot,
+                 sec[5], sec[6], sec[7], (unsigned long long)cnt[2], sec[8], (unsigned long long)rays);
   }
   c->last.kernel_ms = kms;
   c->last.total_ms = all;

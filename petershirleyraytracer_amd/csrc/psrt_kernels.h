@@ -30,6 +30,11 @@ struct BvhView {
   const int* __restrict__ big_idx;       // spheres tested on every ray
   int n_nodes, n_big;
   double r_check;
+  // point-location grid (psrt_bvh.h GridHost)
+  const int* __restrict__ cell_start;
+  const int* __restrict__ cell_items;
+  double glo[3], gcell, ginv, gmargin;
+  int gdims[3];
 };
 
 struct ReduceArgs {

@@ -139,12 +139,22 @@ __device__ __forceinline__ HitRec hit_record_of(const double4 s, double ir, doub
 // |o| > r_check, A not in (0, 1e200)) take the linear sweep.
 
 // sphere.cc:6-31 for one sphere, then the (t, index) rule of the list scan.
+// Pre-reject (exact): when best_t is finite and the origin lies outside the
+// sphere, every point of the sphere is at least |amc| - r away, so a root needs
+// t*|d| >= |amc| - r = C / (|amc| + r) >= C / sqrt(2 (C + 2 r^2)). If
+// best_t^2 A * 2 (C + 2 r^2) * (1 + 2^-10) < C^2, the sphere's roots lie beyond
+// best_t by a relative margin of ~2^-11, far above the FP64 error of the
+// computed root (~1e-8 relative even at tangency), so it cannot be accepted.
 __device__ __forceinline__ void test_sphere(const double4 s, int idx, double ox, double oy,
                                             double oz, double dx, double dy, double dz,
                                             double A, double& best_t, int& best_i) {
   const double ax = ox - s.x, ay = oy - s.y, az = oz - s.z;
-  const double hb = (dx * ax + dy * ay) + dz * az;
   const double c = ((ax * ax + ay * ay) + az * az) - s.w;
+  if (c > 0.0 && best_t < 1e100) {
+    const double lhs = (best_t * best_t) * A * (2.0 * (c + 2.0 * s.w)) * (1.0 + 0x1p-10);
+    if (lhs < c * c) return;
+  }
+  const double hb = (dx * ax + dy * ay) + dz * az;
   const double disc = hb * hb - A * c;
   if (disc < 0.0) return;
   const double sq = __builtin_sqrt(disc);
@@ -159,6 +169,42 @@ __device__ __forceinline__ void test_sphere(const double4 s, int idx, double ox,
   }
 }
 
+// Point query for a short segment [o, o + bt*d] (the common case: the ray
+// re-hit the sphere it starts on at t ~ 0). Returns 1 if resolved (cell
+// spheres tested, or the segment is outside the grid: no culled sphere can
+// be hit), 0 if the BVH must be walked.
+__device__ __forceinline__ int grid_point_query(const double4* __restrict__ geo,
+                                                const BvhView& bv, int hint, double ox,
+                                                double oy, double oz, double dx, double dy,
+                                                double dz, double A, double& bt, int& bi,
+                                                unsigned& tests) {
+  if (!(bt < 1e100)) return 0;
+  const double m = bv.gmargin;
+  const double o3[3] = {ox, oy, oz}, d3[3] = {dx, dy, dz};
+  int ci[3];
+  bool outside = false;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double e = o3[k] + bt * d3[k];
+    const double lo = __builtin_fmin(o3[k], e) - m, hi = __builtin_fmax(o3[k], e) + m;
+    const double glo = bv.glo[k], ghi = bv.glo[k] + bv.gdims[k] * bv.gcell;
+    if (hi < glo || lo > ghi) outside = true;
+    const int c0 = (int)__builtin_floor((lo - glo) * bv.ginv);
+    const int c1 = (int)__builtin_floor((hi - glo) * bv.ginv);
+    ci[k] = (c0 == c1 && c0 >= 0 && c0 < bv.gdims[k]) ? c0 : -1;
+  }
+  if (outside) return 1;
+  if (ci[0] < 0 || ci[1] < 0 || ci[2] < 0) return 0;
+  const int cell = (ci[2] * bv.gdims[1] + ci[1]) * bv.gdims[0] + ci[0];
+  const int e0 = bv.cell_start[cell], e1 = bv.cell_start[cell + 1];
+  for (int e = e0; e < e1; ++e) {
+    const int idx = bv.cell_items[e];
+    if (idx == hint) continue;
+    test_sphere(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
+    ++tests;
+  }
+  return 1;
+}
 
 __device__ __forceinline__ float tmax_up(double t) {
   // >= t for every finite t (float rounding <= 2^-24 relative; margin 2^-21)
@@ -172,8 +218,16 @@ __device__ __forceinline__ float safe_inv(float d) {
 
 struct CullStats {
   unsigned boxes, spheres;
+  // diagnostic build only: wave-level loop trips (counted by the first
+  // active lane) vs lane-level work, to measure traversal divergence
+  unsigned wave_trips = 0, wave_leaf_trips = 0, trav_rays = 0, leaf_visits = 0;
 };
 
+__device__ __forceinline__ bool first_active_lane() {
+  return __lane_id() == (unsigned)__builtin_ctzll(__ballot(1));
+}
+
+template <bool kDiag>
 __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, int n,
                                              const BvhView& bv, int hint, double ox, double oy,
                                              double oz, double dx, double dy, double dz, double A,
@@ -196,6 +250,10 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
     if (idx != hint) test_sphere(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
   }
   cs.spheres += bv.n_big;
+  if (grid_point_query(geo, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs.spheres)) {
+    best_t = bt;
+    return bi;
+  }
   if (!(am <= bv.r_check)) {
     // Far origin (e.g. inside the r=1000 ground): the FP32 slab bound does not
     // hold. Test [0, bt] against the padded root box in FP64 (error ~1e-13
@@ -229,7 +287,11 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
   const float oix = fox * ix, oiy = foy * iy, oiz = foz * iz;
   float tmax = tmax_up(bt);
   int node = 0;
+  if constexpr (kDiag) ++cs.trav_rays;
   while (node < bv.n_nodes) {
+    if constexpr (kDiag) {
+      if (first_active_lane()) ++cs.wave_trips;
+    }
     const float4 a = bv.nodes[2 * node];
     const float4 b = bv.nodes[2 * node + 1];
     // slab distances; FP32 FMA is fine here: the test only needs to be
@@ -248,6 +310,10 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
         continue;
       }
       const int first = leaf >> 8, cnt = leaf & 255;
+      if constexpr (kDiag) {
+        ++cs.leaf_visits;
+        if (first_active_lane()) ++cs.wave_leaf_trips;
+      }
       for (int k = first; k < first + cnt; ++k) {
         const int idx = bv.leaf_idx[k];
         if (idx == hint) continue;
@@ -347,7 +413,7 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
       } else {
         ++rays;
         if constexpr (kBVH) {
-          hit = world_hit_bvh(geo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, t, cs);
+          hit = world_hit_bvh<kStamps>(geo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, t, cs);
         } else {
           hit = sweep_linear(geo, a.n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), t);
           cs.spheres += a.n;
@@ -400,6 +466,11 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
   if constexpr (kStamps) {
     if (lane == 0)
       for (int k2 = 0; k2 < kSecCount; ++k2) atomicAdd(a.stamps + k2, (unsigned long long)clk.acc[k2]);
+    // wave-level counters live in whichever lane was first active: sum them all
+    atomicAdd(a.stamps + 5, (unsigned long long)cs.wave_trips);
+    atomicAdd(a.stamps + 6, (unsigned long long)cs.wave_leaf_trips);
+    atomicAdd(a.stamps + 7, (unsigned long long)cs.trav_rays);
+    atomicAdd(a.stamps + 8, (unsigned long long)cs.leaf_visits);
   }
 
   // rays / sphere tests / box tests of this wave -> one atomic each
@@ -487,7 +558,7 @@ __global__ void psrt_probe_hit(const double4* __restrict__ geo, const double* __
   int i;
   if (use_bvh && r[6] == 0.0 && r[7] == __builtin_inf()) {  // the trace kernel's call shape
     CullStats cs{0u, 0u};
-    i = world_hit_bvh(geo, n, bv, -1, ox, oy, oz, dx, dy, dz, A, t, cs);
+    i = world_hit_bvh<false>(geo, n, bv, -1, ox, oy, oz, dx, dy, dz, A, t, cs);
   } else {
     i = sweep_linear(geo, n, ox, oy, oz, dx, dy, dz, A, r[6], r[7], t);
   }
