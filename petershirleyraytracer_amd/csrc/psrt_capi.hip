@@ -358,6 +358,11 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   HIP_TRY(hipMemsetAsync(c->d_counters + 1, 0, 31 * sizeof(unsigned long long), st));
   const bool stamps = std::getenv("PSRT_STAMPS") != nullptr;  // diagnostic build
   ta.stamps = c->d_counters + 8;
+  {
+    const char* e = std::getenv("PSRT_BATCH");  // tuning knob (default 24 of 64 lanes)
+    ta.batch = e ? (unsigned)std::atoi(e) : 24u;
+    if (ta.batch < 1) ta.batch = 1;
+  }
   const bool use_bvh = c->bvh && !(p->flags & RT_FLAG_NO_CULL);
   const psrt::BvhView bv = bvh_view(c);
   HIP_TRY(hipEventRecord(c->ev_all0, st));

@@ -21,6 +21,7 @@ struct TraceArgs {
   unsigned long long* work_counter;
   unsigned long long* ray_counter;  // [0] rays, [1] sphere tests, [2] box tests
   unsigned long long* stamps;       // diagnostic build: cycles per section (kSecCount)
+  unsigned batch;                   // parked lanes that trigger a batched BVH pass
 };
 
 struct BvhView {

@@ -139,18 +139,19 @@ __device__ __forceinline__ HitRec hit_record_of(const double4 s, double ir, doub
 // |o| > r_check, A not in (0, 1e200)) take the linear sweep.
 
 // sphere.cc:6-31 for one sphere, then the (t, index) rule of the list scan.
-// Pre-reject (exact): when best_t is finite and the origin lies outside the
-// sphere, every point of the sphere is at least |amc| - r away, so a root needs
-// t*|d| >= |amc| - r = C / (|amc| + r) >= C / sqrt(2 (C + 2 r^2)). If
-// best_t^2 A * 2 (C + 2 r^2) * (1 + 2^-10) < C^2, the sphere's roots lie beyond
-// best_t by a relative margin of ~2^-11, far above the FP64 error of the
-// computed root (~1e-8 relative even at tangency), so it cannot be accepted.
+// Pre-reject (exact): when best_t is finite and the origin lies clearly outside
+// the sphere (C > 2^-10 r^2), every point of the sphere is at least
+// D = |amc| - r = C / (|amc| + r) >= C / sqrt(2 (C + 2 r^2)) away, so a root
+// needs t*|d| >= D. If best_t^2 A * 2 (C + 2 r^2) * (1 + 2^-10) < C^2, every
+// root lies beyond best_t by >= 2^-11 D; the computed root's error (<= ~1.5e-8
+// |amc| even at tangency) is below that because D >= 2^-11 |amc| when
+// C > 2^-10 r^2. Origins nearer the surface always take the full test.
 __device__ __forceinline__ void test_sphere(const double4 s, int idx, double ox, double oy,
                                             double oz, double dx, double dy, double dz,
                                             double A, double& best_t, int& best_i) {
   const double ax = ox - s.x, ay = oy - s.y, az = oz - s.z;
   const double c = ((ax * ax + ay * ay) + az * az) - s.w;
-  if (c > 0.0 && best_t < 1e100) {
+  if (c > 0x1p-10 * s.w && c > 0.0 && best_t < 1e100) {
     const double lhs = (best_t * best_t) * A * (2.0 * (c + 2.0 * s.w)) * (1.0 + 0x1p-10);
     if (lhs < c * c) return;
   }
@@ -227,20 +228,24 @@ __device__ __forceinline__ bool first_active_lane() {
   return __lane_id() == (unsigned)__builtin_ctzll(__ballot(1));
 }
 
-template <bool kDiag>
-__device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, int n,
-                                             const BvhView& bv, int hint, double ox, double oy,
-                                             double oz, double dx, double dy, double dz, double A,
-                                             double& best_t, CullStats& cs) {
+// Cheap part of hittable_list::hit with culling: the previous-hit sphere
+// first, the big spheres, then the point-location grid. Returns true when the
+// closest hit is decided (bt, bi); false when the BVH must be walked (the
+// ray's bt, bi so far stay valid and hit_traverse continues from them).
+__device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo, int n,
+                                          const BvhView& bv, int hint, double ox, double oy,
+                                          double oz, double dx, double dy, double dz, double A,
+                                          double& bt, int& bi, CullStats& cs) {
+  bt = __builtin_inf();
+  bi = -1;
   const bool finite = (A > 0.0) && (A < 1e200);
   const double am = __builtin_fmax(__builtin_fabs(ox),
                                    __builtin_fmax(__builtin_fabs(oy), __builtin_fabs(oz)));
-  if (!finite || !(am < 1e200)) {
+  if (!finite || !(am < 1e200)) {  // unbounded arithmetic: the reference scan, verbatim
     cs.spheres += n;
-    return sweep_linear(geo, n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), best_t);
+    bi = sweep_linear(geo, n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), bt);
+    return true;
   }
-  double bt = __builtin_inf();
-  int bi = -1;
   if (hint >= 0) {
     test_sphere(geo[hint], hint, ox, oy, oz, dx, dy, dz, A, bt, bi);
     ++cs.spheres;
@@ -250,10 +255,7 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
     if (idx != hint) test_sphere(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
   }
   cs.spheres += bv.n_big;
-  if (grid_point_query(geo, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs.spheres)) {
-    best_t = bt;
-    return bi;
-  }
+  if (grid_point_query(geo, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs.spheres)) return true;
   if (!(am <= bv.r_check)) {
     // Far origin (e.g. inside the r=1000 ground): the FP32 slab bound does not
     // hold. Test [0, bt] against the padded root box in FP64 (error ~1e-13
@@ -277,11 +279,19 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
     ++cs.boxes;
     if (t0 <= t1 * (1.0 + 0x1p-40) + 0x1p-40) {
       cs.spheres += n;
-      return sweep_linear(geo, n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), best_t);
+      bi = sweep_linear(geo, n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), bt);
     }
-    best_t = bt;
-    return bi;
+    return true;
   }
+  return false;
+}
+
+// The BVH walk (stackless, skip links) for a bounded ray, continuing from the
+// (bt, bi) hit_quick left.
+template <bool kDiag>
+__device__ __forceinline__ void hit_traverse(const BvhView& bv, int hint, double ox, double oy,
+                                             double oz, double dx, double dy, double dz,
+                                             double A, double& bt, int& bi, CullStats& cs) {
   const float fox = (float)ox, foy = (float)oy, foz = (float)oz;
   const float ix = safe_inv((float)dx), iy = safe_inv((float)dy), iz = safe_inv((float)dz);
   const float oix = fox * ix, oiy = foy * iy, oiz = foz * iz;
@@ -324,6 +334,17 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
     }
     node = skip;
   }
+}
+
+// hittable_list::hit(r, 0, +inf) with culling, one lane (probe kernel).
+__device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, int n,
+                                             const BvhView& bv, int hint, double ox, double oy,
+                                             double oz, double dx, double dy, double dz, double A,
+                                             double& best_t, CullStats& cs) {
+  double bt;
+  int bi;
+  if (!hit_quick(geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs))
+    hit_traverse<false>(bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs);
   best_t = bt;
   return bi;
 }
@@ -349,6 +370,9 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
   unsigned sl = 0;    // sample index within the chunk
   unsigned rays = 0;
   int hint = -1;  // sphere the ray starts on (the previous hit), tested first
+  bool pending = false;  // parked for the next batched BVH pass
+  double pbt = 0.0;      // closest t / index so far of this ray's world.hit
+  int pbi = -1;
   CullStats cs{0u, 0u};
   SectionClock<kStamps> clk;
   clk.start();
@@ -403,29 +427,46 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
     if (__ballot(active) == 0) break;
 
     // ---- world.hit(r, 0, inf, rec)  (main.cc:40) ----
-    int hit = -1;
-    double t = 0.0;
-    bool finish = false;
+    // Cheap part for every live, non-parked lane; rays that need the BVH walk
+    // park (pending) and are walked together in one batched pass once enough
+    // lanes wait (or nothing else can progress): the pass then runs at high
+    // SIMD occupancy instead of once per iteration for a handful of lanes.
+    bool resolved = false, finish = false;
     double col_r = 0.0, col_g = 0.0, col_b = 0.0;
-    if (active) {
+    if (active && !pending) {
       if (a.max_depth < 0) {  // main.cc:36-37 at the first call: black, no trace
         finish = true;
       } else {
         ++rays;
         if constexpr (kBVH) {
-          hit = world_hit_bvh<kStamps>(geo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, t, cs);
+          resolved = hit_quick(geo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi, cs);
+          pending = !resolved;
         } else {
-          hit = sweep_linear(geo, a.n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), t);
+          pbi = sweep_linear(geo, a.n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), pbt);
           cs.spheres += a.n;
+          resolved = true;
         }
-        // depth-0 hit: 0.5 * ray_color(.., -1) = black (main.cc:36-37, 43)
-        if (hit < 0 || k >= a.max_depth) finish = true;
       }
     }
+    if constexpr (kBVH) {
+      const uint64_t pend = __ballot(pending);
+      const uint64_t movable = __ballot(active && !pending);
+      if (pend != 0 && ((unsigned)__popcll(pend) >= a.batch || movable == 0)) {
+        if (pending) {
+          hit_traverse<kStamps>(bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi, cs);
+          pending = false;
+          resolved = true;
+        }
+      }
+    }
+    // depth-0 hit: 0.5 * ray_color(.., -1) = black (main.cc:36-37, 43)
+    if (resolved && (pbi < 0 || k >= a.max_depth)) finish = true;
+    const int hit = pbi;
+    const double t = pbt;
     clk.mark(kSecHit);
 
     // ---- scatter: target = (p + n) + random_in_hemisphere(n)  (main.cc:42-43) ----
-    if (active && !finish) {
+    if (resolved && !finish) {
       const HitRec h = hit_record_of(geo[hit], inv_r[hit], t, ox, oy, oz, dx, dy, dz);
       // vec3.h:83-95 (g++ order: z, y, x) and vec3.h:102-109
       double rx, ry, rz;
@@ -446,7 +487,7 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
     clk.mark(kSecScatter);
 
     // ---- sample done: sky (main.cc:46-48) x 0.5^k, or black; store ----
-    if (active && finish) {
+    if (finish) {
       if (hit < 0 && a.max_depth >= 0) {
         const double y = (1.0 / __builtin_sqrt(A)) * dy;
         const double tt = 0.5 * (y + 1.0);
@@ -558,7 +599,7 @@ __global__ void psrt_probe_hit(const double4* __restrict__ geo, const double* __
   int i;
   if (use_bvh && r[6] == 0.0 && r[7] == __builtin_inf()) {  // the trace kernel's call shape
     CullStats cs{0u, 0u};
-    i = world_hit_bvh<false>(geo, n, bv, -1, ox, oy, oz, dx, dy, dz, A, t, cs);
+    i = world_hit_bvh(geo, n, bv, -1, ox, oy, oz, dx, dy, dz, A, t, cs);
   } else {
     i = sweep_linear(geo, n, ox, oy, oz, dx, dy, dz, A, r[6], r[7], t);
   }
