@@ -359,9 +359,12 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   const bool stamps = std::getenv("PSRT_STAMPS") != nullptr;  // diagnostic build
   ta.stamps = c->d_counters + 8;
   {
-    const char* e = std::getenv("PSRT_BATCH");  // tuning knob (default 24 of 64 lanes)
-    ta.batch = e ? (unsigned)std::atoi(e) : 24u;
+    const char* e = std::getenv("PSRT_BATCH");  // tuning knob (default 20 of 64 lanes)
+    ta.batch = e ? (unsigned)std::atoi(e) : 20u;
     if (ta.batch < 1) ta.batch = 1;
+    const char* f = std::getenv("PSRT_RNG_FILL");  // tuning knob (default 2)
+    ta.rng_fill = f ? std::atoi(f) : 2;
+    if (ta.rng_fill < 0) ta.rng_fill = 0;
   }
   const bool use_bvh = c->bvh && !(p->flags & RT_FLAG_NO_CULL);
   const psrt::BvhView bv = bvh_view(c);
@@ -436,8 +439,8 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
     double tot = 0;
     for (int k = 0; k < 5; ++k) tot += (double)sec[k];
     std::fprintf(stderr,
-                 "{\"psrt_sections\": {\"refill\": %.4f, \"hit\": %.4f, \"scatter\": %.4f, "
-                 "\"shade\": %.4f, \"other\": %.4f, \"wave_cycles\": %.4g, "
+                 "{\"psrt_sections\": {\"refill\": %.4f, \"hit_quick\": %.4f, \"scatter\": %.4f, "
+                 "\"fill_shade\": %.4f, \"traverse\": %.4f, \"wave_cycles\": %.4g, "
                  "\"wave_trips\": %llu, \"wave_leaf_trips\": %llu, \"trav_rays\": %llu, "
                  "\"lane_boxes\": %llu, \"leaf_visits\": %llu, \"rays\": %llu}}\n",
                  sec[0] / tot, sec[1] / tot, sec[2] / tot, sec[3] / tot, sec[4] / tot, tot,

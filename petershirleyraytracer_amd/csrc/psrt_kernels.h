@@ -22,6 +22,7 @@ struct TraceArgs {
   unsigned long long* ray_counter;  // [0] rays, [1] sphere tests, [2] box tests
   unsigned long long* stamps;       // diagnostic build: cycles per section (kSecCount)
   unsigned batch;                   // parked lanes that trigger a batched BVH pass
+  int rng_fill;                     // look-ahead trials per lane per iteration (min)
 };
 
 struct BvhView {

@@ -31,7 +31,7 @@ __device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
 // Diagnostic build only (kStamps): wave-level cycle accounting per kernel
 // section, one s_memtime per boundary (cdna_hip_programming.md §7 stamps).
 // Read its SHARES, never its run time.
-enum Section { kSecRefill = 0, kSecHit, kSecScatter, kSecShade, kSecOther, kSecCount };
+enum Section { kSecRefill = 0, kSecHit, kSecScatter, kSecFillShade, kSecTraverse, kSecCount };
 
 template <bool kOn>
 struct SectionClock {
@@ -139,21 +139,24 @@ __device__ __forceinline__ HitRec hit_record_of(const double4 s, double ir, doub
 // |o| > r_check, A not in (0, 1e200)) take the linear sweep.
 
 // sphere.cc:6-31 for one sphere, then the (t, index) rule of the list scan.
-// Pre-reject (exact): when best_t is finite and the origin lies clearly outside
-// the sphere (C > 2^-10 r^2), every point of the sphere is at least
-// D = |amc| - r = C / (|amc| + r) >= C / sqrt(2 (C + 2 r^2)) away, so a root
-// needs t*|d| >= D. If best_t^2 A * 2 (C + 2 r^2) * (1 + 2^-10) < C^2, every
-// root lies beyond best_t by >= 2^-11 D; the computed root's error (<= ~1.5e-8
-// |amc| even at tangency) is below that because D >= 2^-11 |amc| when
-// C > 2^-10 r^2. Origins nearer the surface always take the full test.
+// Pre-reject (exact): when best_t is finite and the origin lies outside the
+// sphere, every point of the sphere is at least
+// D = |amc| - r = C / (|amc| + r) >= C / sqrt(2 (C + 2 r^2)) away, so any root
+// has t*|d| >= D. The computed root's spatial error is <= ~2^-25 |amc| (worst
+// case: tangency, where the discriminant's rounding error is ~2^-52 HALF_B^2).
+// If best_t^2 A * 2 (C + 2 r^2) * (1 + 2^-4) < C^2, every root lies beyond
+// best_t by >= 2^-5 D; that gap exceeds the root error whenever
+// D >= 2^-17 |amc|, guaranteed by C^2 >= 2^-33 (C + r^2)(C + 2 r^2). Origins
+// nearer the surface always take the full test.
 __device__ __forceinline__ void test_sphere(const double4 s, int idx, double ox, double oy,
                                             double oz, double dx, double dy, double dz,
                                             double A, double& best_t, int& best_i) {
   const double ax = ox - s.x, ay = oy - s.y, az = oz - s.z;
   const double c = ((ax * ax + ay * ay) + az * az) - s.w;
-  if (c > 0x1p-10 * s.w && c > 0.0 && best_t < 1e100) {
-    const double lhs = (best_t * best_t) * A * (2.0 * (c + 2.0 * s.w)) * (1.0 + 0x1p-10);
-    if (lhs < c * c) return;
+  if (c > 0.0 && best_t < 1e100) {
+    const double c2 = c * c, k2 = 2.0 * (c + 2.0 * s.w);
+    if (c2 >= 0x1p-34 * (c + s.w) * k2 && (best_t * best_t) * A * k2 * (1.0 + 0x1p-4) < c2)
+      return;
   }
   const double hb = (dx * ax + dy * ay) + dz * az;
   const double disc = hb * hb - A * c;
@@ -371,6 +374,10 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
   unsigned rays = 0;
   int hint = -1;  // sphere the ray starts on (the previous hit), tested first
   bool pending = false;  // parked for the next batched BVH pass
+  // look-ahead of random_in_unit_sphere (vec3.h:83-95): accepted trials, in
+  // stream order, as raw rand() triples (z, y, x draw order)
+  uint32_t q0x = 0, q0y = 0, q0z = 0, q1x = 0, q1y = 0, q1z = 0;
+  int qn = 0;
   double pbt = 0.0;      // closest t / index so far of this ray's world.hit
   int pbi = -1;
   CullStats cs{0u, 0u};
@@ -411,6 +418,7 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
           A = (dx * dx + dy * dy) + dz * dz;
           k = 0;
           hint = -1;
+          qn = 0;  // the sample's stream starts here: no look-ahead yet
           active = true;
         }
       }
@@ -448,6 +456,7 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
         }
       }
     }
+    clk.mark(kSecHit);
     if constexpr (kBVH) {
       const uint64_t pend = __ballot(pending);
       const uint64_t movable = __ballot(active && !pending);
@@ -463,18 +472,44 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
     if (resolved && (pbi < 0 || k >= a.max_depth)) finish = true;
     const int hit = pbi;
     const double t = pbt;
-    clk.mark(kSecHit);
+    clk.mark(kSecTraverse);
+
+    // ---- random_in_unit_sphere look-ahead (vec3.h:83-95) ----
+    // Each sample draws from its own stream, so the trials of its next bounces
+    // can be generated early, in stream order, and queued; a lane that ends its
+    // sample just drops its queue (those draws would never have been made, and
+    // no other sample's stream depends on them). Every live lane tops up its
+    // queue each iteration, converged; the loop runs longer only while a lane
+    // that scatters now has nothing queued.
+    {
+      const bool want = resolved && !finish;
+      const bool can_fill = active && !finish;
+      for (int f = 0;; ++f) {
+        if (f >= a.rng_fill && __ballot(want && qn == 0) == 0) break;
+        if (can_fill && qn < 2) {
+          const uint32_t z = rand31(rng), y = rand31(rng), x = rand31(rng);
+          const double rz = -1.0 + 2.0 * ((double)z * 0x1p-31);
+          const double ry = -1.0 + 2.0 * ((double)y * 0x1p-31);
+          const double rx = -1.0 + 2.0 * ((double)x * 0x1p-31);
+          if (!((rx * rx + ry * ry) + rz * rz > 1.0)) {
+            if (qn == 0) q0x = x, q0y = y, q0z = z;
+            else q1x = x, q1y = y, q1z = z;
+            ++qn;
+          }
+        }
+      }
+    }
+    clk.mark(kSecFillShade);
 
     // ---- scatter: target = (p + n) + random_in_hemisphere(n)  (main.cc:42-43) ----
     if (resolved && !finish) {
       const HitRec h = hit_record_of(geo[hit], inv_r[hit], t, ox, oy, oz, dx, dy, dz);
-      // vec3.h:83-95 (g++ order: z, y, x) and vec3.h:102-109
-      double rx, ry, rz;
-      do {
-        rz = random_pm1(rng);
-        ry = random_pm1(rng);
-        rx = random_pm1(rng);
-      } while ((rx * rx + ry * ry) + rz * rz > 1.0);
+      // vec3.h:78-81 random(-1, 1) from the queued draws; vec3.h:102-109 flip
+      double rx = -1.0 + 2.0 * ((double)q0x * 0x1p-31);
+      double ry = -1.0 + 2.0 * ((double)q0y * 0x1p-31);
+      double rz = -1.0 + 2.0 * ((double)q0z * 0x1p-31);
+      q0x = q1x, q0y = q1y, q0z = q1z;
+      --qn;
       if (!((rx * h.nx + ry * h.ny) + rz * h.nz > 0.0)) rx = -rx, ry = -ry, rz = -rz;
       dx = ((h.px + h.nx) + rx) - h.px;
       dy = ((h.py + h.ny) + ry) - h.py;
@@ -502,7 +537,7 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
       dst[2] = col_b;
       active = false;
     }
-    clk.mark(kSecShade);
+    clk.mark(kSecFillShade);
   }
   if constexpr (kStamps) {
     if (lane == 0)
