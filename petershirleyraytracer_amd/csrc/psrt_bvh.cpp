@@ -190,20 +190,27 @@ BvhHost build_bvh(const rt_sphere* s, int n) {
   double cell = std::max(2.5 * median, ext / 128.0);
   if (!(cell > 0)) cell = std::max(ext, 1.0);
   GridHost& g = out.grid;
-  g.cell = cell;
+  g.finv = (float)(1.0 / cell);
+  const double inv = (double)g.finv;  // the cell size actually used: 1/finv
   long ncell = 1;
   for (int k = 0; k < 3; ++k) {
-    g.lo[k] = all.lo[k];
-    g.dims[k] = std::max(1, (int)std::ceil((all.hi[k] - all.lo[k]) / cell));
+    g.flo[k] = down(all.lo[k]);
+    g.dims[k] = std::max(1, (int)std::ceil((all.hi[k] - (double)g.flo[k]) * inv) + 1);
+    g.fhi[k] = up((double)g.flo[k] + g.dims[k] / inv);
     ncell *= g.dims[k];
   }
   std::vector<std::vector<int32_t>> cells((size_t)ncell);
   auto cidx = [&](int x, int y, int z) { return ((long)z * g.dims[1] + y) * g.dims[0] + x; };
+  // conservative membership: a sphere joins every cell its padded box touches,
+  // boundaries included (the box is widened by 2^-30 of the scale first)
+  const double eps = std::ldexp(scale, -30);
   for (const Prim& p : prims) {
     int c0[3], c1[3];
     for (int k = 0; k < 3; ++k) {
-      c0[k] = std::max(0, std::min(g.dims[k] - 1, (int)std::floor((p.box.lo[k] - g.lo[k]) / cell)));
-      c1[k] = std::max(0, std::min(g.dims[k] - 1, (int)std::floor((p.box.hi[k] - g.lo[k]) / cell)));
+      const double a = std::floor((p.box.lo[k] - eps - (double)g.flo[k]) * inv);
+      const double b = std::floor((p.box.hi[k] + eps - (double)g.flo[k]) * inv);
+      c0[k] = (int)std::max(0.0, std::min((double)g.dims[k] - 1, a));
+      c1[k] = (int)std::max(0.0, std::min((double)g.dims[k] - 1, b));
     }
     for (int z = c0[2]; z <= c1[2]; ++z)
       for (int y = c0[1]; y <= c1[1]; ++y)

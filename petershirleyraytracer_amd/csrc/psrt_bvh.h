@@ -38,8 +38,11 @@ constexpr int kLeafMax = 2;
 // cell can only hit those spheres (its hit point is inside the hit sphere's
 // padded box and inside the cell).
 struct GridHost {
-  double lo[3] = {0, 0, 0};
-  double cell = 1.0;
+  // The device computes cell indices in FP32 from exactly these constants;
+  // cell c on axis k spans [flo + c/finv, flo + (c+1)/finv] (exact reals).
+  float flo[3] = {0, 0, 0};
+  float fhi[3] = {0, 0, 0};  // >= flo + dims/finv: the grid's outer bound
+  float finv = 1.0f;
   int dims[3] = {0, 0, 0};
   std::vector<int32_t> start;  // dims[0]*dims[1]*dims[2] + 1 offsets into items
   std::vector<int32_t> items;  // original sphere indices

@@ -282,13 +282,16 @@ static psrt::BvhView bvh_view(const rt_context* c) {
   v.r_check = c->r_check;
   v.cell_start = c->d_cell_start;
   v.cell_items = c->d_cell_items;
+  // grid bounds / scale in FP32, as used: the cell index of the device is a
+  // function of these exact float values, and the host places each sphere in
+  // every cell its padded box overlaps under the SAME float cell boundaries
   for (int k = 0; k < 3; ++k) {
-    v.glo[k] = c->pgrid.lo[k];
+    v.glo[k] = c->pgrid.flo[k];
+    v.ghi[k] = c->pgrid.fhi[k];
     v.gdims[k] = c->pgrid.dims[k];
   }
-  v.gcell = c->pgrid.cell;
-  v.ginv = 1.0 / c->pgrid.cell;
-  v.gmargin = c->pad * 0.25;
+  v.ginv = c->pgrid.finv;
+  v.gmargin = (float)(c->pad * 0.25);
   return v;
 }
 

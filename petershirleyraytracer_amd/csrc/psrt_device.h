@@ -38,4 +38,12 @@ __device__ __forceinline__ double random_pm1(uint64_t& st) {
   return -1.0 + 2.0 * random_double(st);
 }
 
+// The same value from a raw rand() draw x: -1 + 2*(x*2^-31) is the exact
+// value (2x - 2^31) * 2^-31 (at most 32 significant bits, so neither the
+// reference's product nor its sum rounds); int -> double and the power-of-two
+// scale are exact too.
+__device__ __forceinline__ double pm1_of(uint32_t x) {
+  return (double)(int)(2u * x - 0x80000000u) * 0x1p-31;
+}
+
 }  // namespace psrt

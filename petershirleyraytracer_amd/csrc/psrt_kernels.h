@@ -35,7 +35,7 @@ struct BvhView {
   // point-location grid (psrt_bvh.h GridHost)
   const int* __restrict__ cell_start;
   const int* __restrict__ cell_items;
-  double glo[3], gcell, ginv, gmargin;
+  float glo[3], ghi[3], ginv, gmargin;  // FP32 copies (conservative use only)
   int gdims[3];
 };
 

@@ -182,19 +182,23 @@ __device__ __forceinline__ int grid_point_query(const double4* __restrict__ geo,
                                                 double oy, double oz, double dx, double dy,
                                                 double dz, double A, double& bt, int& bi,
                                                 unsigned& tests) {
-  if (!(bt < 1e100)) return 0;
-  const double m = bv.gmargin;
-  const double o3[3] = {ox, oy, oz}, d3[3] = {dx, dy, dz};
+  if (!(bt < 1e30)) return 0;
+  // FP32 is enough: the test is conservative and its error (~2^-22 of the
+  // scene scale) is far inside the margin (pad/4, psrt_bvh.cpp)
+  const float m = bv.gmargin;
+  const float o3[3] = {(float)ox, (float)oy, (float)oz};
+  const float d3[3] = {(float)dx, (float)dy, (float)dz};
+  const float tb = (float)bt * 1.00000048f;
   int ci[3];
   bool outside = false;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const double e = o3[k] + bt * d3[k];
-    const double lo = __builtin_fmin(o3[k], e) - m, hi = __builtin_fmax(o3[k], e) + m;
-    const double glo = bv.glo[k], ghi = bv.glo[k] + bv.gdims[k] * bv.gcell;
+    const float e = __builtin_fmaf(tb, d3[k], o3[k]);
+    const float lo = fminf(o3[k], e) - m, hi = fmaxf(o3[k], e) + m;
+    const float glo = bv.glo[k], ghi = bv.ghi[k];
     if (hi < glo || lo > ghi) outside = true;
-    const int c0 = (int)__builtin_floor((lo - glo) * bv.ginv);
-    const int c1 = (int)__builtin_floor((hi - glo) * bv.ginv);
+    const int c0 = (int)__builtin_floorf((lo - glo) * bv.ginv);
+    const int c1 = (int)__builtin_floorf((hi - glo) * bv.ginv);
     ci[k] = (c0 == c1 && c0 >= 0 && c0 < bv.gdims[k]) ? c0 : -1;
   }
   if (outside) return 1;
@@ -488,9 +492,7 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
         if (f >= a.rng_fill && __ballot(want && qn == 0) == 0) break;
         if (can_fill && qn < 2) {
           const uint32_t z = rand31(rng), y = rand31(rng), x = rand31(rng);
-          const double rz = -1.0 + 2.0 * ((double)z * 0x1p-31);
-          const double ry = -1.0 + 2.0 * ((double)y * 0x1p-31);
-          const double rx = -1.0 + 2.0 * ((double)x * 0x1p-31);
+          const double rz = pm1_of(z), ry = pm1_of(y), rx = pm1_of(x);
           if (!((rx * rx + ry * ry) + rz * rz > 1.0)) {
             if (qn == 0) q0x = x, q0y = y, q0z = z;
             else q1x = x, q1y = y, q1z = z;
@@ -505,9 +507,7 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
     if (resolved && !finish) {
       const HitRec h = hit_record_of(geo[hit], inv_r[hit], t, ox, oy, oz, dx, dy, dz);
       // vec3.h:78-81 random(-1, 1) from the queued draws; vec3.h:102-109 flip
-      double rx = -1.0 + 2.0 * ((double)q0x * 0x1p-31);
-      double ry = -1.0 + 2.0 * ((double)q0y * 0x1p-31);
-      double rz = -1.0 + 2.0 * ((double)q0z * 0x1p-31);
+      double rx = pm1_of(q0x), ry = pm1_of(q0y), rz = pm1_of(q0z);
       q0x = q1x, q0y = q1y, q0z = q1z;
       --qn;
       if (!((rx * h.nx + ry * h.ny) + rz * h.nz > 0.0)) rx = -rx, ry = -ry, rz = -rz;
