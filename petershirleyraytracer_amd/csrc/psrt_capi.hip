@@ -158,10 +158,10 @@ int rt_context_create(int device, rt_context** out) {
   HIP_TRY(hipGetDeviceProperties(&prop, device));
   c->cus = prop.multiProcessorCount;
   int per_cu = 0;
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace<false, false>,
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace<false, false, false>,
                                                         psrt::kTraceBlock, 0));
   c->grid = c->cus * (per_cu < 1 ? 1 : per_cu);
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace<true, false>,
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace<true, false, true>,
                                                         psrt::kTraceBlock, 0));
   c->grid_bvh = c->cus * (per_cu < 1 ? 1 : per_cu);
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -362,8 +362,8 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   const bool stamps = std::getenv("PSRT_STAMPS") != nullptr;  // diagnostic build
   ta.stamps = c->d_counters + 8;
   {
-    const char* e = std::getenv("PSRT_BATCH");  // tuning knob (default 20 of 64 lanes)
-    ta.batch = e ? (unsigned)std::atoi(e) : 20u;
+    const char* e = std::getenv("PSRT_BATCH");  // tuning knob (default 24 of 64 lanes)
+    ta.batch = e ? (unsigned)std::atoi(e) : 24u;
     if (ta.batch < 1) ta.batch = 1;
     const char* f = std::getenv("PSRT_RNG_FILL");  // tuning knob (default 2)
     ta.rng_fill = f ? std::atoi(f) : 2;
@@ -383,18 +383,19 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     const double4* g4 = c->d_geo;
     const double* ir = c->d_inv_r;
     const dim3 blk(psrt::kTraceBlock);
-    if (use_bvh && !stamps)
-      hipLaunchKernelGGL((psrt::psrt_trace<true, false>), dim3(c->grid_bvh), blk, 0, st, g4, ir,
-                         c->d_samples, ta, bv);
-    else if (use_bvh)
-      hipLaunchKernelGGL((psrt::psrt_trace<true, true>), dim3(c->grid_bvh), blk, 0, st, g4, ir,
-                         c->d_samples, ta, bv);
-    else if (!stamps)
-      hipLaunchKernelGGL((psrt::psrt_trace<false, false>), dim3(c->grid), blk, 0, st, g4, ir,
-                         c->d_samples, ta, bv);
+    const bool lds = c->n_nodes <= psrt::kLdsNodes && !std::getenv("PSRT_NO_LDS");
+    auto launch = [&](auto kern, int grid) {
+      hipLaunchKernelGGL(kern, dim3(grid), blk, 0, st, g4, ir, c->d_samples, ta, bv);
+    };
+    if (!use_bvh)
+      stamps ? launch(psrt::psrt_trace<false, true, false>, c->grid)
+             : launch(psrt::psrt_trace<false, false, false>, c->grid);
+    else if (lds)
+      stamps ? launch(psrt::psrt_trace<true, true, true>, c->grid_bvh)
+             : launch(psrt::psrt_trace<true, false, true>, c->grid_bvh);
     else
-      hipLaunchKernelGGL((psrt::psrt_trace<false, true>), dim3(c->grid), blk, 0, st, g4, ir,
-                         c->d_samples, ta, bv);
+      stamps ? launch(psrt::psrt_trace<true, true, false>, c->grid_bvh)
+             : launch(psrt::psrt_trace<true, false, false>, c->grid_bvh);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[2 * ch + 1], st));
     psrt::ReduceArgs ra{};

@@ -8,6 +8,7 @@ namespace psrt {
 
 constexpr int kTraceBlock = 256;     // 4 waves per workgroup
 constexpr unsigned kWorkChunk = 1024;  // units a wave takes per queue dequeue
+constexpr int kLdsNodes = 640;         // BVH nodes staged per workgroup (20 KB of LDS)
 
 struct TraceArgs {
   int n;               // spheres (geo: {cx, cy, cz, r*r}, inv_r: 1.0/r)
@@ -49,7 +50,7 @@ struct ReduceArgs {
   unsigned char* rgb8;    // [pixels][3] or nullptr (last chunk only)
 };
 
-template <bool kBVH, bool kStamps>
+template <bool kBVH, bool kStamps, bool kLds>
 __global__ void psrt_trace(const double4* __restrict__ geo, const double* __restrict__ inv_r,
                            double* __restrict__ samples, TraceArgs a, BvhView bv);
 __global__ void psrt_reduce(ReduceArgs a);

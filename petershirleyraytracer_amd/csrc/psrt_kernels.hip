@@ -296,7 +296,8 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo, int n
 // The BVH walk (stackless, skip links) for a bounded ray, continuing from the
 // (bt, bi) hit_quick left.
 template <bool kDiag>
-__device__ __forceinline__ void hit_traverse(const BvhView& bv, int hint, double ox, double oy,
+__device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __restrict__ nodes,
+                                             int hint, double ox, double oy,
                                              double oz, double dx, double dy, double dz,
                                              double A, double& bt, int& bi, CullStats& cs) {
   const float fox = (float)ox, foy = (float)oy, foz = (float)oz;
@@ -309,8 +310,8 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, int hint, double
     if constexpr (kDiag) {
       if (first_active_lane()) ++cs.wave_trips;
     }
-    const float4 a = bv.nodes[2 * node];
-    const float4 b = bv.nodes[2 * node + 1];
+    const float4 a = nodes[2 * node];
+    const float4 b = nodes[2 * node + 1];
     // slab distances; FP32 FMA is fine here: the test only needs to be
     // conservative, and the box padding covers its rounding (psrt_bvh.cpp)
     const float x0 = __builtin_fmaf(a.x, ix, -oix), x1 = __builtin_fmaf(b.x, ix, -oix);
@@ -351,18 +352,27 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
   double bt;
   int bi;
   if (!hit_quick(geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs))
-    hit_traverse<false>(bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs);
+    hit_traverse<false>(bv, bv.nodes, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs);
   best_t = bt;
   return bi;
 }
 
-template <bool kBVH, bool kStamps>
+template <bool kBVH, bool kStamps, bool kLds>
 __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restrict__ geo,
                                                           const double* __restrict__ inv_r,
                                                           double* __restrict__ samples,
                                                           TraceArgs a, BvhView bv) {
   const unsigned lane = lane_id();
   const uint64_t total = a.total_units;
+
+  // BVH nodes staged in LDS when they fit (kLdsNodes x 32 B); the walk's
+  // dependent node loads then see LDS latency instead of L1/L2 latency
+  __shared__ float4 s_nodes[kLds ? 2 * kLdsNodes : 1];
+  if constexpr (kLds) {  // host guarantees n_nodes <= kLdsNodes
+    for (int e = threadIdx.x; e < 2 * bv.n_nodes; e += blockDim.x) s_nodes[e] = bv.nodes[e];
+    __syncthreads();
+  }
+  const float4* __restrict__ nodes = kLds ? s_nodes : bv.nodes;
 
   // wave-uniform work window
   uint64_t win_base = 0;
@@ -466,7 +476,7 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
       const uint64_t movable = __ballot(active && !pending);
       if (pend != 0 && ((unsigned)__popcll(pend) >= a.batch || movable == 0)) {
         if (pending) {
-          hit_traverse<kStamps>(bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi, cs);
+          hit_traverse<kStamps>(bv, nodes, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi, cs);
           pending = false;
           resolved = true;
         }
@@ -563,13 +573,16 @@ __global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restr
   }
 }
 
-#define PSRT_INSTANTIATE(B, S)                                                             \
-  template __global__ void psrt_trace<B, S>(const double4* __restrict__, const double* __restrict__, \
-                                            double* __restrict__, TraceArgs, BvhView);
-PSRT_INSTANTIATE(false, false)
-PSRT_INSTANTIATE(true, false)
-PSRT_INSTANTIATE(false, true)
-PSRT_INSTANTIATE(true, true)
+#define PSRT_INSTANTIATE(B, S, L)                                                          \
+  template __global__ void psrt_trace<B, S, L>(const double4* __restrict__,                 \
+                                               const double* __restrict__, double* __restrict__, \
+                                               TraceArgs, BvhView);
+PSRT_INSTANTIATE(false, false, false)
+PSRT_INSTANTIATE(true, false, false)
+PSRT_INSTANTIATE(true, false, true)
+PSRT_INSTANTIATE(false, true, false)
+PSRT_INSTANTIATE(true, true, false)
+PSRT_INSTANTIATE(true, true, true)
 #undef PSRT_INSTANTIATE
 
 // pixel_color += sample, in sample order (main.cc:77-84); write_color on the
