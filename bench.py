@@ -174,7 +174,8 @@ def main():
     from petershirleyraytracer_amd.render import FLAG_NO_CULL
 
     torch.cuda.set_device(local)
-    if world > 1:
+    distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ or "MASTER_PORT" in os.environ
+    if distributed:  # one process per GPU over RCCL (backend "nccl" on ROCm)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     w, h, spp = cfg["width"], cfg["height"], cfg["spp"]
@@ -191,7 +192,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     def barrier():
-        if world > 1:
+        if distributed:
             dist.barrier()
 
     kernel_ms, rays, executed, elapsed = [], [], [], 0.0
@@ -203,7 +204,7 @@ def main():
             t0 = time.perf_counter()
         if world == 1:
             ctx.render_device(prm, acc.data_ptr(), rgb.data_ptr(), stream.cuda_stream)
-            frame = acc
+            frame = gather_frame(acc, h, rank, world) if distributed else acc
         else:
             ctx.render_device(prm, acc.data_ptr(), 0, stream.cuda_stream)
             frame = gather_frame(acc, h, rank, world)
@@ -218,7 +219,7 @@ def main():
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -301,7 +302,7 @@ def main():
         print(json.dumps(out), flush=True)
 
     ctx.close()
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 
