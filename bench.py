@@ -95,12 +95,13 @@ def cpu_baseline(cfg, args, frame_acc):
     # per-core reference rate: two-sphere 0.62 Ms/s, final 0.0232 Ms/s
     rate = 0.62e6 if cfg["scene"] == "two" else 0.0232e6
     want_samples = args.cpu_seconds * procs * rate
-    rows = max(1, min(h, int(want_samples / (w * spp))))
+    # rows spread over the whole frame; at most 100 spp per pixel (a sample's
+    # cost does not depend on spp, and every pixel's first samples are the same
+    # stream prefix), so very high spp still sees the frame's real mix of rays
+    spp_eff = min(spp, 100)
+    rows = max(1, min(h, int(want_samples / (w * spp_eff))))
     stride = max(1, h // rows)
     rows = len(range(0, h, stride))
-    spp_eff = spp
-    if rows == 1 and w * spp > want_samples:  # very high spp: shorten the sample count
-        spp_eff = max(1, int(want_samples / w))
     cols = np.linspace(0, w, procs + 1).astype(int)
     with tempfile.TemporaryDirectory() as td:
         cmds = []
