@@ -65,14 +65,15 @@ def load(build_if_missing: bool = False):
         import torch  # noqa: F401
     except ImportError:
         pass
-    if not os.path.exists(LIB):
+    lib_path = os.environ.get("PSRT_LIB", LIB)  # A/B builds (tuning only)
+    if not os.path.exists(lib_path):
         if build_if_missing:
             from .build import build_lib
             build_lib()
         else:
             raise RtError(f"libpsrt.so not built ({LIB}); run __graft_entry__.build() or "
                           f"python -m petershirleyraytracer_amd.build")
-    L = C.CDLL(LIB)
+    L = C.CDLL(lib_path)
     P = C.POINTER
     sig = {
         "rt_rows_owned": ([C.c_int, C.c_int, C.c_int], C.c_int),

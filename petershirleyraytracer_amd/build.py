@@ -47,16 +47,18 @@ def _deps():
     return out
 
 
-def build_lib(force: bool = False, verbose: bool = False) -> str:
+def build_lib(force: bool = False, verbose: bool = False, out: str = LIB,
+              defines=()) -> str:
     os.makedirs(LIB_DIR, exist_ok=True)
     srcs = [os.path.join(CSRC, s) for s in LIB_SOURCES]
-    if not force and _newer(LIB, _deps()):
-        return LIB
-    cmd = [HIPCC, f"--offload-arch={ARCH}", *COMMON, "-fPIC", "-shared", "-o", LIB, *srcs]
+    if not force and _newer(out, _deps()):
+        return out
+    cmd = [HIPCC, f"--offload-arch={ARCH}", *COMMON, *[f"-D{d}" for d in defines], "-fPIC",
+           "-shared", "-o", out, *srcs]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)
-    return LIB
+    return out
 
 
 def build_host(force: bool = False, verbose: bool = False) -> str:

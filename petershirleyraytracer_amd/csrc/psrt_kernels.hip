@@ -221,7 +221,7 @@ __device__ __forceinline__ float tmax_up(double t) {
 
 __device__ __forceinline__ float safe_inv(float d) {
   const float m = __builtin_fabsf(d) < 1e-20f ? __builtin_copysignf(1e-20f, d) : d;
-  return 1.0f / m;
+  return __builtin_amdgcn_rcpf(m);  // v_rcp_f32 (1 ulp): the padded boxes absorb it
 }
 
 struct CullStats {
@@ -277,7 +277,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo, int n
       if (d3[k] == 0.0) {
         if (o3[k] < lo3[k] || o3[k] > hi3[k]) t0 = 2.0, t1 = 1.0;  // parallel, outside
       } else {
-        const double inv = 1.0 / d3[k];
+        const double inv = __builtin_amdgcn_rcp(d3[k]);  // v_rcp_f64; error << the pad
         const double u = (lo3[k] - o3[k]) * inv, v = (hi3[k] - o3[k]) * inv;
         t0 = __builtin_fmax(t0, __builtin_fmin(u, v));
         t1 = __builtin_fmin(t1, __builtin_fmax(u, v));
@@ -357,8 +357,13 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
   return bi;
 }
 
+#ifndef PSRT_TRACE_WAVES
+#define PSRT_TRACE_WAVES 6  // min waves per SIMD requested from the register allocator
+                            // (6: 80 VGPRs, +2% over 5 despite 4 spilled VGPRs; 7 loses)
+#endif
+
 template <bool kBVH, bool kStamps, bool kLds>
-__global__ __launch_bounds__(kTraceBlock) void psrt_trace(const double4* __restrict__ geo,
+__global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(const double4* __restrict__ geo,
                                                           const double* __restrict__ inv_r,
                                                           double* __restrict__ samples,
                                                           TraceArgs a, BvhView bv) {
