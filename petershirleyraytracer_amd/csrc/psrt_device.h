@@ -27,6 +27,28 @@ __device__ __forceinline__ uint32_t rand31(uint64_t& st) {
   return ((xs >> rot) | (xs << ((32u - rot) & 31u))) >> 1;
 }
 
+// XSH-RR output of a PCG32 state (the value rand31 returns for `old`), >> 1.
+__device__ __forceinline__ uint32_t pcg_out31(uint64_t old) {
+  const uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
+  const uint32_t rot = (uint32_t)(old >> 59);
+  return ((xs >> rot) | (xs << ((32u - rot) & 31u))) >> 1;
+}
+
+// Three consecutive draws with the LCG jumped ahead: s1 = a s0 + c,
+// s2 = a^2 s0 + c (a + 1), s3 = a^3 s0 + c (a^2 + a + 1) (mod 2^64) — the same
+// values as three rand31() calls, from independent multiplies. Returns the
+// state after the third draw in `next`.
+__device__ __forceinline__ void rand31_x3(uint64_t s0, uint32_t& r0, uint32_t& r1,
+                                          uint32_t& r2, uint64_t& next) {
+  const uint64_t s1 = s0 * 6364136223846793005ULL + 1442695040888963407ULL;
+  const uint64_t s2 = s0 * 0x685f98a2018fade9ULL + 0x1a08ee1184ba6d32ULL;
+  const uint64_t s3 = s0 * 0x0b046976f22528f5ULL + 0x9af678222e728119ULL;
+  r0 = pcg_out31(s0);
+  r1 = pcg_out31(s1);
+  r2 = pcg_out31(s2);
+  next = s3;
+}
+
 // random_double(): (double)rand() / (RAND_MAX + 1.0). The divisor is 2^31, so
 // the quotient is exact and equals the product with 2^-31.
 __device__ __forceinline__ double random_double(uint64_t& st) {

@@ -503,17 +503,22 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     {
       const bool want = resolved && !finish;
       const bool can_fill = active && !finish;
+      // branch-free body: every lane computes a trial; only lanes with room
+      // take it (their stream advances), so the draws stay in stream order
       for (int f = 0;; ++f) {
         if (f >= a.rng_fill && __ballot(want && qn == 0) == 0) break;
-        if (can_fill && qn < 2) {
-          const uint32_t z = rand31(rng), y = rand31(rng), x = rand31(rng);
-          const double rz = pm1_of(z), ry = pm1_of(y), rx = pm1_of(x);
-          if (!((rx * rx + ry * ry) + rz * rz > 1.0)) {
-            if (qn == 0) q0x = x, q0y = y, q0z = z;
-            else q1x = x, q1y = y, q1z = z;
-            ++qn;
-          }
-        }
+        const bool go = can_fill && qn < 2;
+        uint32_t z, y, x;
+        uint64_t nxt;
+        rand31_x3(rng, z, y, x, nxt);  // z, y, x: g++'s draw order (vec3.h:78-81)
+        const double rz = pm1_of(z), ry = pm1_of(y), rx = pm1_of(x);
+        const bool in = !((rx * rx + ry * ry) + rz * rz > 1.0);
+        rng = go ? nxt : rng;
+        const bool push = go && in;
+        const bool to0 = push && qn == 0, to1 = push && qn == 1;
+        q0x = to0 ? x : q0x, q0y = to0 ? y : q0y, q0z = to0 ? z : q0z;
+        q1x = to1 ? x : q1x, q1y = to1 ? y : q1y, q1z = to1 ? z : q1z;
+        qn += push ? 1 : 0;
       }
     }
     clk.mark(kSecFillShade);
