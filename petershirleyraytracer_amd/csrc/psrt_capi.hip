@@ -438,20 +438,20 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   c->last.tests_executed = cnt[1];
   c->last.box_tests = cnt[2];
   if (std::getenv("PSRT_STAMPS")) {
-    unsigned long long sec[9];
+    unsigned long long sec[12];
     HIP_TRY(hipMemcpy(sec, c->d_counters + 8, sizeof sec, hipMemcpyDeviceToHost));
     double tot = 0;
-    for (int k = 0; k < 5; ++k) tot += (double)sec[k];
+    for (int k = 0; k < 8; ++k) tot += (double)sec[k];
     std::fprintf(stderr,
-                 "{\"psrt_sections\": {\"refill\": %.4f, \"hit_quick\": %.4f, \"scatter\": %.4f, "
+                 "{\"psrt_sections\": {\"refill\": %.4f, \"hit_quick\": %.4f, "
+                 "\"q_hint\": %.4f, \"q_big\": %.4f, \"q_grid\": %.4f, \"scatter\": %.4f, "
                  "\"fill_shade\": %.4f, \"traverse\": %.4f, \"wave_cycles\": %.4g, "
                  "\"wave_trips\": %llu, \"wave_leaf_trips\": %llu, \"trav_rays\": %llu, "
                  "\"lane_boxes\": %llu, \"leaf_visits\": %llu, \"rays\": %llu}}\n",
-                 sec[0] / tot, sec[1] / tot, sec[2] / tot, sec[3] / tot, sec[4] / tot, tot,
-                 sec[5], sec[6], sec[7], (unsigned long long)cnt[2], sec[8], (unsigned long long)rays);
+                 sec[0] / tot, sec[1] / tot, sec[5] / tot, sec[6] / tot, sec[7] / tot,
+                 sec[2] / tot, sec[3] / tot, sec[4] / tot, tot, sec[8], sec[9], sec[10],
+                 (unsigned long long)cnt[2], sec[11], (unsigned long long)rays);
   }
-  c->last.kernel_ms = kms;
-  c->last.total_ms = all;
   if (s) *s = c->last;
   return RT_OK;
 }

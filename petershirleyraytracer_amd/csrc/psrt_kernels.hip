@@ -31,11 +31,14 @@ __device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
 // Diagnostic build only (kStamps): wave-level cycle accounting per kernel
 // section, one s_memtime per boundary (cdna_hip_programming.md §7 stamps).
 // Read its SHARES, never its run time.
-enum Section { kSecRefill = 0, kSecHit, kSecScatter, kSecFillShade, kSecTraverse, kSecCount };
+enum Section {
+  kSecRefill = 0, kSecHit, kSecScatter, kSecFillShade, kSecTraverse,
+  kSecQHint, kSecQBig, kSecQGrid, kSecCount  // hit_quick sub-sections (share of kSecHit)
+};
 
 template <bool kOn>
 struct SectionClock {
-  uint64_t t = 0, acc[kSecCount] = {0, 0, 0, 0, 0};
+  uint64_t t = 0, acc[kSecCount] = {0, 0, 0, 0, 0, 0, 0, 0};
   __device__ __forceinline__ void start() {
     if constexpr (kOn) t = now();
   }
@@ -239,10 +242,15 @@ __device__ __forceinline__ bool first_active_lane() {
 // first, the big spheres, then the point-location grid. Returns true when the
 // closest hit is decided (bt, bi); false when the BVH must be walked (the
 // ray's bt, bi so far stay valid and hit_traverse continues from them).
+__device__ __forceinline__ double root_box_entry(const BvhView& bv, double ox, double oy,
+                                                 double oz, double dx, double dy, double dz,
+                                                 double tmax);
+
+template <class Clock>
 __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo, int n,
                                           const BvhView& bv, int hint, double ox, double oy,
                                           double oz, double dx, double dy, double dz, double A,
-                                          double& bt, int& bi, CullStats& cs) {
+                                          double& bt, int& bi, CullStats& cs, Clock& clk) {
   bt = __builtin_inf();
   bi = -1;
   const bool finite = (A > 0.0) && (A < 1e200);
@@ -257,40 +265,48 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo, int n
     test_sphere(geo[hint], hint, ox, oy, oz, dx, dy, dz, A, bt, bi);
     ++cs.spheres;
   }
+  clk.mark(kSecQHint);
   for (int b = 0; b < bv.n_big; ++b) {
     const int idx = bv.big_idx[b];
     if (idx != hint) test_sphere(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
   }
   cs.spheres += bv.n_big;
-  if (grid_point_query(geo, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs.spheres)) return true;
+  clk.mark(kSecQBig);
+  const bool done = grid_point_query(geo, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs.spheres);
+  clk.mark(kSecQGrid);
+  if (done) return true;
   if (!(am <= bv.r_check)) {
-    // Far origin (e.g. inside the r=1000 ground): the FP32 slab bound does not
-    // hold. Test [0, bt] against the padded root box in FP64 (error ~1e-13
-    // relative, far inside the pad): a miss proves no BVH sphere can have a
-    // root in [0, bt]; a hit takes the exact linear sweep.
-    const float4 ra = bv.nodes[0], rb = bv.nodes[1];
-    double t0 = 0.0, t1 = bt;
-    const double o3[3] = {ox, oy, oz}, d3[3] = {dx, dy, dz};
-    const double lo3[3] = {ra.x, ra.y, ra.z}, hi3[3] = {rb.x, rb.y, rb.z};
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      if (d3[k] == 0.0) {
-        if (o3[k] < lo3[k] || o3[k] > hi3[k]) t0 = 2.0, t1 = 1.0;  // parallel, outside
-      } else {
-        const double inv = __builtin_amdgcn_rcp(d3[k]);  // v_rcp_f64; error << the pad
-        const double u = (lo3[k] - o3[k]) * inv, v = (hi3[k] - o3[k]) * inv;
-        t0 = __builtin_fmax(t0, __builtin_fmin(u, v));
-        t1 = __builtin_fmin(t1, __builtin_fmax(u, v));
-      }
-    }
+    // Far origin (e.g. inside the r=1000 ground): test [0, bt] against the
+    // padded root box in FP64 (error ~1e-13 relative, far inside the pad). A
+    // miss proves no BVH sphere can have a root in [0, bt]; a hit parks the
+    // ray for the batched walk, which re-bases it at the box entry (hit_traverse).
     ++cs.boxes;
-    if (t0 <= t1 * (1.0 + 0x1p-40) + 0x1p-40) {
-      cs.spheres += n;
-      bi = sweep_linear(geo, n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), bt);
-    }
-    return true;
+    if (root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt) < 0.0) return true;
   }
   return false;
+}
+
+// Entry t in [0, tmax] of the ray into the padded BVH root box, in FP64;
+// negative if the segment misses the box.
+__device__ __forceinline__ double root_box_entry(const BvhView& bv, double ox, double oy,
+                                                 double oz, double dx, double dy, double dz,
+                                                 double tmax) {
+  const float4 ra = bv.nodes[0], rb = bv.nodes[1];
+  double t0 = 0.0, t1 = tmax;
+  const double o3[3] = {ox, oy, oz}, d3[3] = {dx, dy, dz};
+  const double lo3[3] = {ra.x, ra.y, ra.z}, hi3[3] = {rb.x, rb.y, rb.z};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (d3[k] == 0.0) {
+      if (o3[k] < lo3[k] || o3[k] > hi3[k]) t0 = 2.0, t1 = 1.0;  // parallel, outside
+    } else {
+      const double inv = __builtin_amdgcn_rcp(d3[k]);  // v_rcp_f64; error << the pad
+      const double u = (lo3[k] - o3[k]) * inv, v = (hi3[k] - o3[k]) * inv;
+      t0 = __builtin_fmax(t0, __builtin_fmin(u, v));
+      t1 = __builtin_fmin(t1, __builtin_fmax(u, v));
+    }
+  }
+  return (t0 <= t1 * (1.0 + 0x1p-40) + 0x1p-40) ? t0 : -1.0;
 }
 
 // The BVH walk (stackless, skip links) for a bounded ray, continuing from the
@@ -300,10 +316,19 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
                                              int hint, double ox, double oy,
                                              double oz, double dx, double dy, double dz,
                                              double A, double& bt, int& bi, CullStats& cs) {
-  const float fox = (float)ox, foy = (float)oy, foz = (float)oz;
+  // Far origins are re-based at their root-box entry o' = o + t0 d (FP64), so
+  // the FP32 slab test sees |o'| <= the scene scale and its error bound holds;
+  // box intervals are then tested over [-t0, bt - t0]. The exact sphere tests
+  // in the leaves keep the original o.
+  double t0 = 0.0;
+  const double am = __builtin_fmax(__builtin_fabs(ox),
+                                   __builtin_fmax(__builtin_fabs(oy), __builtin_fabs(oz)));
+  if (!(am <= bv.r_check)) t0 = __builtin_fmax(0.0, root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt));
+  const float fox = (float)(ox + t0 * dx), foy = (float)(oy + t0 * dy), foz = (float)(oz + t0 * dz);
   const float ix = safe_inv((float)dx), iy = safe_inv((float)dy), iz = safe_inv((float)dz);
   const float oix = fox * ix, oiy = foy * iy, oiz = foz * iz;
-  float tmax = tmax_up(bt);
+  const float tlo = -(float)t0 * 1.00000048f;  // <= -t0: the ray's t >= 0
+  float tmax = tmax_up(bt - t0);
   int node = 0;
   if constexpr (kDiag) ++cs.trav_rays;
   while (node < bv.n_nodes) {
@@ -317,7 +342,7 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
     const float x0 = __builtin_fmaf(a.x, ix, -oix), x1 = __builtin_fmaf(b.x, ix, -oix);
     const float y0 = __builtin_fmaf(a.y, iy, -oiy), y1 = __builtin_fmaf(b.y, iy, -oiy);
     const float z0 = __builtin_fmaf(a.z, iz, -oiz), z1 = __builtin_fmaf(b.z, iz, -oiz);
-    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.0f));
+    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tlo));
     const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tmax));
     ++cs.boxes;
     const int skip = __float_as_int(a.w);
@@ -338,7 +363,7 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
         test_sphere(bv.leaf_geo[k], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
         ++cs.spheres;
       }
-      tmax = tmax_up(bt);
+      tmax = tmax_up(bt - t0);
     }
     node = skip;
   }
@@ -351,7 +376,8 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
                                              double& best_t, CullStats& cs) {
   double bt;
   int bi;
-  if (!hit_quick(geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs))
+  SectionClock<false> noclk;
+  if (!hit_quick(geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs, noclk))
     hit_traverse<false>(bv, bv.nodes, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs);
   best_t = bt;
   return bi;
@@ -466,7 +492,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       } else {
         ++rays;
         if constexpr (kBVH) {
-          resolved = hit_quick(geo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi, cs);
+          resolved = hit_quick(geo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi, cs, clk);
           pending = !resolved;
         } else {
           pbi = sweep_linear(geo, a.n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), pbt);
@@ -563,10 +589,10 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     if (lane == 0)
       for (int k2 = 0; k2 < kSecCount; ++k2) atomicAdd(a.stamps + k2, (unsigned long long)clk.acc[k2]);
     // wave-level counters live in whichever lane was first active: sum them all
-    atomicAdd(a.stamps + 5, (unsigned long long)cs.wave_trips);
-    atomicAdd(a.stamps + 6, (unsigned long long)cs.wave_leaf_trips);
-    atomicAdd(a.stamps + 7, (unsigned long long)cs.trav_rays);
-    atomicAdd(a.stamps + 8, (unsigned long long)cs.leaf_visits);
+    atomicAdd(a.stamps + 8, (unsigned long long)cs.wave_trips);
+    atomicAdd(a.stamps + 9, (unsigned long long)cs.wave_leaf_trips);
+    atomicAdd(a.stamps + 10, (unsigned long long)cs.trav_rays);
+    atomicAdd(a.stamps + 11, (unsigned long long)cs.leaf_visits);
   }
 
   // rays / sphere tests / box tests of this wave -> one atomic each
