@@ -437,6 +437,8 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   c->last.sphere_tests = rays * (uint64_t)(c->n_last > 0 ? c->n_last : 0);
   c->last.tests_executed = cnt[1];
   c->last.box_tests = cnt[2];
+  c->last.kernel_ms = kms;
+  c->last.total_ms = all;
   if (std::getenv("PSRT_STAMPS")) {
     unsigned long long sec[12];
     HIP_TRY(hipMemcpy(sec, c->d_counters + 8, sizeof sec, hipMemcpyDeviceToHost));

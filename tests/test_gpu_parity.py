@@ -102,6 +102,7 @@ def test_counter_two_sphere_fixtures():
         assert hashlib.md5(P.ppm_p3(rgb)).hexdigest() == c["p3_md5"], c
         assert st["rays"] == c["rays"], c
         assert st["samples"] == acc.shape[0] * acc.shape[1] * c["spp"]
+        assert 0 < st["kernel_ms"] <= st["total_ms"], st
 
 
 def test_counter_final_fixtures(final_scene):
