@@ -383,7 +383,8 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     const double4* g4 = c->d_geo;
     const double* ir = c->d_inv_r;
     const dim3 blk(psrt::kTraceBlock);
-    const bool lds = c->n_nodes <= psrt::kLdsNodes && !std::getenv("PSRT_NO_LDS");
+    const bool lds = c->n_nodes <= psrt::kLdsNodes && c->n <= psrt::kLdsSpheres &&
+                     !std::getenv("PSRT_NO_LDS");
     auto launch = [&](auto kern, int grid) {
       hipLaunchKernelGGL(kern, dim3(grid), blk, 0, st, g4, ir, c->d_samples, ta, bv);
     };

@@ -6,9 +6,10 @@
 
 namespace psrt {
 
-constexpr int kTraceBlock = 256;     // 4 waves per workgroup
+constexpr int kTraceBlock = 512;     // 8 waves per workgroup (3 per CU share 160 KB of LDS)
 constexpr unsigned kWorkChunk = 1024;  // units a wave takes per queue dequeue
 constexpr int kLdsNodes = 640;         // BVH nodes staged per workgroup (20 KB of LDS)
+constexpr int kLdsSpheres = 640;       // spheres staged per workgroup (25 KB of LDS)
 
 struct TraceArgs {
   int n;               // spheres (geo: {cx, cy, cz, r*r}, inv_r: 1.0/r)

@@ -180,7 +180,7 @@ __device__ __forceinline__ void test_sphere(const double4 s, int idx, double ox,
 // re-hit the sphere it starts on at t ~ 0). Returns 1 if resolved (cell
 // spheres tested, or the segment is outside the grid: no culled sphere can
 // be hit), 0 if the BVH must be walked.
-__device__ __forceinline__ int grid_point_query(const double4* __restrict__ geo,
+__device__ __forceinline__ int grid_point_query(const double4* __restrict__ lgeo,
                                                 const BvhView& bv, int hint, double ox,
                                                 double oy, double oz, double dx, double dy,
                                                 double dz, double A, double& bt, int& bi,
@@ -211,7 +211,7 @@ __device__ __forceinline__ int grid_point_query(const double4* __restrict__ geo,
   for (int e = e0; e < e1; ++e) {
     const int idx = bv.cell_items[e];
     if (idx == hint) continue;
-    test_sphere(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
+    test_sphere(lgeo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
     ++tests;
   }
   return 1;
@@ -247,7 +247,8 @@ __device__ __forceinline__ double root_box_entry(const BvhView& bv, double ox, d
                                                  double tmax);
 
 template <class Clock>
-__device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo, int n,
+__device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
+                                          const double4* __restrict__ lgeo, int n,
                                           const BvhView& bv, int hint, double ox, double oy,
                                           double oz, double dx, double dy, double dz, double A,
                                           double& bt, int& bi, CullStats& cs, Clock& clk) {
@@ -262,7 +263,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo, int n
     return true;
   }
   if (hint >= 0) {
-    test_sphere(geo[hint], hint, ox, oy, oz, dx, dy, dz, A, bt, bi);
+    test_sphere(lgeo[hint], hint, ox, oy, oz, dx, dy, dz, A, bt, bi);
     ++cs.spheres;
   }
   clk.mark(kSecQHint);
@@ -272,7 +273,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo, int n
   }
   cs.spheres += bv.n_big;
   clk.mark(kSecQBig);
-  const bool done = grid_point_query(geo, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs.spheres);
+  const bool done = grid_point_query(lgeo, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs.spheres);
   clk.mark(kSecQGrid);
   if (done) return true;
   if (!(am <= bv.r_check)) {
@@ -377,7 +378,7 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
   double bt;
   int bi;
   SectionClock<false> noclk;
-  if (!hit_quick(geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs, noclk))
+  if (!hit_quick(geo, geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs, noclk))
     hit_traverse<false>(bv, bv.nodes, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs);
   best_t = bt;
   return bi;
@@ -398,12 +399,19 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
 
   // BVH nodes staged in LDS when they fit (kLdsNodes x 32 B); the walk's
   // dependent node loads then see LDS latency instead of L1/L2 latency
+  // With kLds, the spheres (geo, 1/r) are staged as well: the per-lane gathers
+  // (previous-hit test, grid cell items, the hit record) then read LDS.
   __shared__ float4 s_nodes[kLds ? 2 * kLdsNodes : 1];
-  if constexpr (kLds) {  // host guarantees n_nodes <= kLdsNodes
+  __shared__ double4 s_geo[kLds ? kLdsSpheres : 1];
+  __shared__ double s_inv[kLds ? kLdsSpheres : 1];
+  if constexpr (kLds) {  // host guarantees n_nodes <= kLdsNodes and n <= kLdsSpheres
     for (int e = threadIdx.x; e < 2 * bv.n_nodes; e += blockDim.x) s_nodes[e] = bv.nodes[e];
+    for (int e = threadIdx.x; e < a.n; e += blockDim.x) s_geo[e] = geo[e], s_inv[e] = inv_r[e];
     __syncthreads();
   }
   const float4* __restrict__ nodes = kLds ? s_nodes : bv.nodes;
+  const double4* __restrict__ lgeo = kLds ? s_geo : geo;
+  const double* __restrict__ linv = kLds ? s_inv : inv_r;
 
   // wave-uniform work window
   uint64_t win_base = 0;
@@ -492,7 +500,8 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       } else {
         ++rays;
         if constexpr (kBVH) {
-          resolved = hit_quick(geo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi, cs, clk);
+          resolved =
+              hit_quick(geo, lgeo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi, cs, clk);
           pending = !resolved;
         } else {
           pbi = sweep_linear(geo, a.n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), pbt);
@@ -551,7 +560,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
 
     // ---- scatter: target = (p + n) + random_in_hemisphere(n)  (main.cc:42-43) ----
     if (resolved && !finish) {
-      const HitRec h = hit_record_of(geo[hit], inv_r[hit], t, ox, oy, oz, dx, dy, dz);
+      const HitRec h = hit_record_of(lgeo[hit], linv[hit], t, ox, oy, oz, dx, dy, dz);
       // vec3.h:78-81 random(-1, 1) from the queued draws; vec3.h:102-109 flip
       double rx = pm1_of(q0x), ry = pm1_of(q0y), rz = pm1_of(q0z);
       q0x = q1x, q0y = q1y, q0z = q1z;
