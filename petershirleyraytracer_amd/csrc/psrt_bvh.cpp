@@ -181,6 +181,15 @@ BvhHost build_bvh(const rt_sphere* s, int n) {
   }
   Builder bld{prims, out};
   bld.build(0, (int)prims.size(), 0);
+  // padding node (never reached: the walk stops at nodes.size()); lets the
+  // device read node+1 speculatively. Empty box, leaf word -1, skip = end.
+  {
+    BvhNode pad{};
+    for (int k = 0; k < 3; ++k) pad.lo[k] = 1.0f, pad.hi[k] = -1.0f;
+    pad.skip = (int32_t)out.nodes.size();
+    pad.leaf = -1;
+    out.nodes.push_back(pad);
+  }
 
   // point-location grid: cells ~2.5 median radii wide, at most 128 per axis
   Box all;

@@ -50,7 +50,7 @@ struct GridHost {
 
 struct BvhHost {
   GridHost grid;
-  std::vector<BvhNode> nodes;
+  std::vector<BvhNode> nodes;  // DFS order + one trailing padding node
   std::vector<int32_t> leaf_idx;  // original sphere index per leaf slot
   std::vector<int32_t> big_idx;   // original indices tested on every ray
   double pad = 0.0;               // absolute box padding

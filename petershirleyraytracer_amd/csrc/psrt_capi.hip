@@ -238,7 +238,7 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
   c->bvh = b.enabled;
   c->n_nodes = c->n_big = c->n_leaf = 0;
   if (b.enabled) {
-    c->n_nodes = (int)b.nodes.size();
+    c->n_nodes = (int)b.nodes.size() - 1;  // the walk's node count (excl. padding)
     c->n_big = (int)b.big_idx.size();
     c->n_leaf = (int)b.leaf_idx.size();
     c->r_check = b.r_check;
@@ -383,7 +383,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     const double4* g4 = c->d_geo;
     const double* ir = c->d_inv_r;
     const dim3 blk(psrt::kTraceBlock);
-    const bool lds = c->n_nodes <= psrt::kLdsNodes && c->n <= psrt::kLdsSpheres &&
+    const bool lds = c->n_nodes + 1 <= psrt::kLdsNodes && c->n <= psrt::kLdsSpheres &&
                      !std::getenv("PSRT_NO_LDS");
     auto launch = [&](auto kern, int grid) {
       hipLaunchKernelGGL(kern, dim3(grid), blk, 0, st, g4, ir, c->d_samples, ta, bv);

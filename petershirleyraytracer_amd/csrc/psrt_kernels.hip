@@ -227,6 +227,18 @@ __device__ __forceinline__ float safe_inv(float d) {
   return __builtin_amdgcn_rcpf(m);  // v_rcp_f32 (1 ulp): the padded boxes absorb it
 }
 
+// Conservative FP32 ray-box test over [tlo, tmax] (boxes padded, psrt_bvh.cpp).
+__device__ __forceinline__ bool slab_hit(const float4 lo, const float4 hi, float ix, float iy,
+                                         float iz, float oix, float oiy, float oiz, float tlo,
+                                         float tmax) {
+  const float x0 = __builtin_fmaf(lo.x, ix, -oix), x1 = __builtin_fmaf(hi.x, ix, -oix);
+  const float y0 = __builtin_fmaf(lo.y, iy, -oiy), y1 = __builtin_fmaf(hi.y, iy, -oiy);
+  const float z0 = __builtin_fmaf(lo.z, iz, -oiz), z1 = __builtin_fmaf(hi.z, iz, -oiz);
+  const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tlo));
+  const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tmax));
+  return tn <= tf;
+}
+
 struct CullStats {
   unsigned boxes, spheres;
   // diagnostic build only: wave-level loop trips (counted by the first
@@ -332,27 +344,38 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
   float tmax = tmax_up(bt - t0);
   int node = 0;
   if constexpr (kDiag) ++cs.trav_rays;
+  // Two nodes per trip: in DFS skip-link order an interior hit always
+  // continues at node+1, so node+1 is loaded and box-tested alongside node
+  // (independent work that overlaps the node-load latency); the trip then
+  // advances two levels when node is an interior hit. Node n_nodes is a padding
+  // node (psrt_bvh.cpp), so node+1 is always readable.
   while (node < bv.n_nodes) {
     if constexpr (kDiag) {
       if (first_active_lane()) ++cs.wave_trips;
     }
-    const float4 a = nodes[2 * node];
-    const float4 b = nodes[2 * node + 1];
+    const float4 a0 = nodes[2 * node], a1 = nodes[2 * node + 1];
+    const float4 b0 = nodes[2 * node + 2], b1 = nodes[2 * node + 3];
     // slab distances; FP32 FMA is fine here: the test only needs to be
     // conservative, and the box padding covers its rounding (psrt_bvh.cpp)
-    const float x0 = __builtin_fmaf(a.x, ix, -oix), x1 = __builtin_fmaf(b.x, ix, -oix);
-    const float y0 = __builtin_fmaf(a.y, iy, -oiy), y1 = __builtin_fmaf(b.y, iy, -oiy);
-    const float z0 = __builtin_fmaf(a.z, iz, -oiz), z1 = __builtin_fmaf(b.z, iz, -oiz);
-    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tlo));
-    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tmax));
-    ++cs.boxes;
-    const int skip = __float_as_int(a.w);
-    const int leaf = __float_as_int(b.w);
-    if (tn <= tf) {
-      if (leaf < 0) {
-        ++node;
-        continue;
-      }
+    const bool hit_a = slab_hit(a0, a1, ix, iy, iz, oix, oiy, oiz, tlo, tmax);
+    const bool hit_b = slab_hit(b0, b1, ix, iy, iz, oix, oiy, oiz, tlo, tmax);
+    cs.boxes += 2;
+    const int leaf_a = __float_as_int(a1.w), leaf_b = __float_as_int(b1.w);
+    int next, leaf = -1;
+    if (!hit_a) {
+      next = __float_as_int(a0.w);
+    } else if (leaf_a >= 0) {
+      leaf = leaf_a;
+      next = __float_as_int(a0.w);
+    } else if (!hit_b) {
+      next = __float_as_int(b0.w);
+    } else if (leaf_b >= 0) {
+      leaf = leaf_b;
+      next = __float_as_int(b0.w);
+    } else {
+      next = node + 2;
+    }
+    if (leaf >= 0) {
       const int first = leaf >> 8, cnt = leaf & 255;
       if constexpr (kDiag) {
         ++cs.leaf_visits;
@@ -366,7 +389,7 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
       }
       tmax = tmax_up(bt - t0);
     }
-    node = skip;
+    node = next;
   }
 }
 
@@ -405,7 +428,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   __shared__ double4 s_geo[kLds ? kLdsSpheres : 1];
   __shared__ double s_inv[kLds ? kLdsSpheres : 1];
   if constexpr (kLds) {  // host guarantees n_nodes <= kLdsNodes and n <= kLdsSpheres
-    for (int e = threadIdx.x; e < 2 * bv.n_nodes; e += blockDim.x) s_nodes[e] = bv.nodes[e];
+    for (int e = threadIdx.x; e < 2 * (bv.n_nodes + 1); e += blockDim.x) s_nodes[e] = bv.nodes[e];
     for (int e = threadIdx.x; e < a.n; e += blockDim.x) s_geo[e] = geo[e], s_inv[e] = inv_r[e];
     __syncthreads();
   }

@@ -29,7 +29,8 @@ static void check_scene(const std::vector<rt_sphere>& s) {
   for (int i : b.big_idx) seen[i] += 1;
   for (int i : b.leaf_idx) seen[i] += 1;
   for (int i = 0; i < n; ++i) CHECK(seen[i] == 1, "every sphere in exactly one leaf or the big list");
-  const int m = (int)b.nodes.size();
+  const int m = (int)b.nodes.size() - 1;  // last node is padding
+  CHECK(b.nodes[m].leaf == -1 && b.nodes[m].lo[0] > b.nodes[m].hi[0], "padding node is empty");
   CHECK(b.nodes[0].skip == m, "root skip == end");
   // walk: every node's subtree is [k+1, skip); leaves own slots; boxes nest
   for (int k = 0; k < m; ++k) {
