@@ -92,6 +92,56 @@ inline frame render(const hittable_list& world, const camera& cam, int width, in
   return f;
 }
 
+// ---- scene files (rt_scene_load; DESIGN.md §Scene files) --------------------
+struct scene_file {
+  std::vector<rt_sphere> spheres;  // hittable_list order
+  rt_camera cam{};
+  rt_params params{};  // width/height/spp/max_depth/seed as the file states
+};
+
+inline scene_file load_scene(const std::string& path, const rt_params& defaults = rt_params{}) {
+  scene_file s;
+  s.params = defaults;
+  rt_params scratch = defaults;
+  const int n = rt_scene_load(path.c_str(), nullptr, 0, &s.cam, &scratch);
+  if (n < 0) check(n, "rt_scene_load");
+  s.spheres.resize(n);
+  check(rt_scene_load(path.c_str(), s.spheres.data(), n, &s.cam, &s.params) < 0
+            ? RT_E_SCENE : RT_OK,
+        "rt_scene_load");
+  return s;
+}
+
+inline std::string format_scene(const std::vector<rt_sphere>& spheres, const rt_camera& cam,
+                                const rt_params* params = nullptr) {
+  const long long len =
+      rt_scene_format(spheres.data(), (int)spheres.size(), &cam, params, nullptr, 0);
+  if (len < 0) check((int)len, "rt_scene_format");
+  std::string text((size_t)len + 1, '\0');
+  rt_scene_format(spheres.data(), (int)spheres.size(), &cam, params, &text[0], text.size());
+  text.resize((size_t)len);
+  return text;
+}
+
+// The reference-API world and camera for a loaded scene (hittable_list of
+// spheres in file order; camera with the file's basis).
+inline hittable_list to_world(const std::vector<rt_sphere>& spheres) {
+  hittable_list world;
+  for (const rt_sphere& q : spheres)
+    world.add(make_shared<sphere>(point3(q.cx, q.cy, q.cz), q.r));
+  return world;
+}
+
+inline camera to_camera(const rt_camera& c) {
+  camera cam;
+  cam.origin = point3(c.origin[0], c.origin[1], c.origin[2]);
+  cam.lower_left_corner = point3(c.lower_left[0], c.lower_left[1], c.lower_left[2]);
+  cam.horizontal = vec3(c.horizontal[0], c.horizontal[1], c.horizontal[2]);
+  cam.vertical = vec3(c.vertical[0], c.vertical[1], c.vertical[2]);
+  cam.aspect_ratio = cam.horizontal.length() / cam.vertical.length();
+  return cam;
+}
+
 // "P3\n<w> <rows>\n255\n" then one "r g b" line per pixel (main.cc:70, color.h:21-23)
 inline void write_ppm(std::ostream& out, const frame& f) {
   out << "P3\n" << f.width << ' ' << f.rows << "\n255\n";

@@ -161,6 +161,28 @@ int rt_scene_two_spheres(rt_sphere* out, int cap);
  * diffuse-only. Returns the sphere count; writes at most cap records. */
 int rt_scene_random_spheres(unsigned int seed, rt_sphere* out, int cap);
 
+/* ---- scene files (extension: SURVEY.md §8(f)3) ------------------------------
+ * Text form of main.cc:53-63 (spheres in hittable_list order, camera,
+ * pixel-loop parameters); grammar in psrt_scenefile.cpp and DESIGN.md
+ * §Scene files. Decimal or hex-float numbers; %.17g output round-trips.
+ *
+ * rt_scene_parse / rt_scene_load: returns the sphere count (writes at most
+ * cap records; call again with a larger buffer if it exceeds cap) or
+ * RT_E_SCENE / RT_E_INVALID. cam (optional) receives the file's camera, or
+ * camera() when it has none. params (optional): only the fields the file's
+ * `render` line names are overwritten (width, height, spp, max_depth, seed);
+ * `aspect auto` uses width/height from the file, else from *params. */
+int rt_scene_parse(const char* text, rt_sphere* out, int cap, rt_camera* cam,
+                   rt_params* params);
+int rt_scene_load(const char* path, rt_sphere* out, int cap, rt_camera* cam,
+                  rt_params* params);
+
+/* Writes the scene file text (camera as a basis, `render` line only when
+ * params != NULL) into buf (NUL-terminated, truncated to cap-1 chars).
+ * Returns the full text length (snprintf-style) or a negative error. */
+long long rt_scene_format(const rt_sphere* spheres, int n_spheres, const rt_camera* cam,
+                          const rt_params* params, char* buf, size_t cap);
+
 /* ---- misc ----------------------------------------------------------------- */
 const char* rt_last_error(void);
 int rt_abi_version(void);

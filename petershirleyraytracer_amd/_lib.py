@@ -19,6 +19,7 @@ EXPORTS = [
     "rt_rows_owned", "rt_render", "rt_quantize_ppm", "rt_context_create", "rt_context_destroy",
     "rt_context_set_scene", "rt_render_device", "rt_context_sync_stats", "rt_quantize_device",
     "rt_camera_default", "rt_camera_look_at", "rt_scene_two_spheres", "rt_scene_random_spheres",
+    "rt_scene_parse", "rt_scene_load", "rt_scene_format",
     "rt_last_error", "rt_abi_version", "rt_device_count", "rt_build_info", "rt_debug_probe_f64",
     "rt_debug_world_hit",
 ]
@@ -93,6 +94,12 @@ def load(build_if_missing: bool = False):
                                C.c_double, P(RtCamera)], C.c_int),
         "rt_scene_two_spheres": ([P(RtSphere), C.c_int], C.c_int),
         "rt_scene_random_spheres": ([C.c_uint, P(RtSphere), C.c_int], C.c_int),
+        "rt_scene_parse": ([C.c_char_p, P(RtSphere), C.c_int, P(RtCamera), P(RtParams)],
+                           C.c_int),
+        "rt_scene_load": ([C.c_char_p, P(RtSphere), C.c_int, P(RtCamera), P(RtParams)],
+                          C.c_int),
+        "rt_scene_format": ([P(RtSphere), C.c_int, P(RtCamera), P(RtParams), C.c_char_p,
+                             C.c_size_t], C.c_longlong),
         "rt_last_error": ([], C.c_char_p),
         "rt_abi_version": ([], C.c_int),
         "rt_device_count": ([], C.c_int),

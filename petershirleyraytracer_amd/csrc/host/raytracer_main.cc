@@ -6,6 +6,9 @@
 //   raytracer                       # main.cc as written: 400 wide, 16:9, 100 spp, depth 50
 //   raytracer --scene final --width 1200 --height 800 --spp 100 -o out.ppm
 //   raytracer --rows 1:8 ...        # one interleaved shard (rows 1, 9, 17, ...)
+//   raytracer --scene-file s.scene  # world/camera/parameters from a scene file;
+//                                   # flags given on the command line win
+//   raytracer --scene final --save-scene final.scene   # write the scene, render nothing
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -42,18 +45,20 @@ void random_spheres(hittable_list& world, unsigned seed) {
 
 int usage() {
   std::fprintf(stderr,
-               "raytracer [--scene two|final] [--width W] [--height H] [--spp S] [--depth D]\n"
-               "          [--seed N] [--rows OFF:STRIDE] [-o FILE] [--p6] [--accum FILE]\n");
+               "raytracer [--scene two|final | --scene-file FILE] [--width W] [--height H]\n"
+               "          [--spp S] [--depth D] [--seed N] [--rows OFF:STRIDE] [-o FILE] [--p6]\n"
+               "          [--accum FILE] [--save-scene FILE]\n");
   return 2;
 }
 
 }  // namespace
 
 int main(int argc, char** argv) {
-  std::string scene = "two", out_path, accum_path;
+  std::string scene = "two", out_path, accum_path, scene_path, save_path;
   int width = 400, height = -1, spp = 100, depth = 50, row_off = 0, row_stride = 1;
   unsigned long long seed = 0;
-  bool p6 = false;
+  bool p6 = false, set_w = false, set_h = false, set_spp = false, set_depth = false,
+       set_seed = false;
   for (int a = 1; a < argc; ++a) {
     const std::string k = argv[a];
     auto val = [&]() -> const char* { return a + 1 < argc ? argv[++a] : nullptr; };
@@ -61,11 +66,13 @@ int main(int argc, char** argv) {
     if (k == "--p6") { p6 = true; continue; }
     if (!(v = val())) return usage();
     if (k == "--scene") scene = v;
-    else if (k == "--width") width = std::atoi(v);
-    else if (k == "--height") height = std::atoi(v);
-    else if (k == "--spp") spp = std::atoi(v);
-    else if (k == "--depth") depth = std::atoi(v);
-    else if (k == "--seed") seed = std::strtoull(v, nullptr, 10);
+    else if (k == "--scene-file") scene_path = v;
+    else if (k == "--save-scene") save_path = v;
+    else if (k == "--width") width = std::atoi(v), set_w = true;
+    else if (k == "--height") height = std::atoi(v), set_h = true;
+    else if (k == "--spp") spp = std::atoi(v), set_spp = true;
+    else if (k == "--depth") depth = std::atoi(v), set_depth = true;
+    else if (k == "--seed") seed = std::strtoull(v, nullptr, 10), set_seed = true;
     else if (k == "-o") out_path = v;
     else if (k == "--accum") accum_path = v;
     else if (k == "--rows") {
@@ -76,7 +83,28 @@ int main(int argc, char** argv) {
   // world + camera (main.cc:53-63)
   hittable_list world;
   camera cam;
-  if (scene == "two") {
+  if (!scene_path.empty()) {
+    try {
+      rt_params defaults{};
+      defaults.width = width;
+      defaults.height = height;
+      defaults.spp = spp;
+      defaults.max_depth = depth;
+      defaults.seed = seed;
+      const psrt::scene_file sf = psrt::load_scene(scene_path, defaults);
+      world = psrt::to_world(sf.spheres);
+      cam = psrt::to_camera(sf.cam);
+      if (!set_w) width = sf.params.width;
+      if (!set_h) height = sf.params.height;
+      if (!set_spp) spp = sf.params.spp;
+      if (!set_depth) depth = sf.params.max_depth;
+      if (!set_seed) seed = sf.params.seed;
+      if (height < 0) height = (int)(width / cam.aspect_ratio);
+    } catch (const std::exception& e) {
+      std::cerr << "raytracer: " << e.what() << "\n";
+      return 1;
+    }
+  } else if (scene == "two") {
     if (height < 0) height = (int)(width / cam.aspect_ratio);
     world.add(make_shared<sphere>(point3(0, 0, -1), 0.5));
     world.add(make_shared<sphere>(point3(0, -100.5, 0), 100.0));
@@ -86,6 +114,24 @@ int main(int argc, char** argv) {
     cam = camera(point3(13, 2, 3), point3(0, 0, 0), vec3(0, 1, 0), 20.0, (double)width / height);
   } else {
     return usage();
+  }
+
+  if (!save_path.empty()) {
+    try {
+      rt_params p{};
+      p.width = width;
+      p.height = height;
+      p.spp = spp;
+      p.max_depth = depth;
+      p.seed = seed;
+      std::ofstream f(save_path, std::ios::binary);
+      f << psrt::format_scene(psrt::flatten(world), psrt::to_rt(cam), &p);
+      if (!f) throw std::runtime_error("cannot write " + save_path);
+    } catch (const std::exception& e) {
+      std::cerr << "raytracer: " << e.what() << "\n";
+      return 1;
+    }
+    return 0;
   }
 
   try {

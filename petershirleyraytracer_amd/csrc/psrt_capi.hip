@@ -17,13 +17,15 @@
 
 #include "../../include/rt.h"
 #include "psrt_bvh.h"
+#include "psrt_error.h"
 #include "psrt_kernels.h"
 
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
 
-int fail(int code, const char* fmt, ...) {
+namespace psrt {
+int set_error(int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;
   va_start(ap, fmt);
@@ -32,12 +34,17 @@ int fail(int code, const char* fmt, ...) {
   g_err = buf;
   return code;
 }
+}  // namespace psrt
+
+namespace {
+
+using psrt::set_error;
 
 #define HIP_TRY(expr)                                                                  \
   do {                                                                                 \
     hipError_t e_ = (expr);                                                            \
     if (e_ != hipSuccess)                                                              \
-      return fail(e_ == hipErrorOutOfMemory ? RT_E_NOMEM : RT_E_HIP, "%s: %s (%s:%d)", \
+      return set_error(e_ == hipErrorOutOfMemory ? RT_E_NOMEM : RT_E_HIP, "%s: %s (%s:%d)", \
                   #expr, hipGetErrorString(e_), __FILE__, __LINE__);                   \
   } while (0)
 
@@ -144,13 +151,13 @@ int rt_rows_owned(int height, int row_offset, int row_stride) {
 }
 
 int rt_context_create(int device, rt_context** out) {
-  if (!out) return fail(RT_E_INVALID, "rt_context_create: out is NULL");
+  if (!out) return set_error(RT_E_INVALID, "rt_context_create: out is NULL");
   *out = nullptr;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
-    return fail(RT_E_NODEVICE, "rt_context_create: no HIP device visible");
+    return set_error(RT_E_NODEVICE, "rt_context_create: no HIP device visible");
   if (device < 0 || device >= ndev)
-    return fail(RT_E_INVALID, "rt_context_create: device %d out of range [0,%d)", device, ndev);
+    return set_error(RT_E_INVALID, "rt_context_create: device %d out of range [0,%d)", device, ndev);
   HIP_TRY(hipSetDevice(device));
   rt_context* c = new rt_context();
   c->device = device;
@@ -197,7 +204,7 @@ int rt_context_destroy(rt_context* c) {
 
 int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_camera* cam) {
   if (!c || !cam || n < 0 || (n > 0 && !sph))
-    return fail(RT_E_INVALID, "rt_context_set_scene: bad arguments");
+    return set_error(RT_E_INVALID, "rt_context_set_scene: bad arguments");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
   const int cap = n > 0 ? n : 1;
@@ -296,27 +303,27 @@ static psrt::BvhView bvh_view(const rt_context* c) {
 }
 
 static int check_params(const rt_params* p) {
-  if (!p) return fail(RT_E_INVALID, "params is NULL");
+  if (!p) return set_error(RT_E_INVALID, "params is NULL");
   if (p->width < 2 || p->height < 2)
-    return fail(RT_E_INVALID, "width/height must be >= 2 (got %d x %d)", p->width, p->height);
-  if (p->spp < 1) return fail(RT_E_INVALID, "spp must be >= 1 (got %d)", p->spp);
+    return set_error(RT_E_INVALID, "width/height must be >= 2 (got %d x %d)", p->width, p->height);
+  if (p->spp < 1) return set_error(RT_E_INVALID, "spp must be >= 1 (got %d)", p->spp);
   if (p->max_depth < -1 || p->max_depth > 100000)
-    return fail(RT_E_INVALID, "max_depth out of range (got %d)", p->max_depth);
+    return set_error(RT_E_INVALID, "max_depth out of range (got %d)", p->max_depth);
   if (p->row_stride < 1 || p->row_offset < 0 || p->row_offset >= p->height)
-    return fail(RT_E_INVALID, "bad shard: row_offset %d row_stride %d height %d", p->row_offset,
+    return set_error(RT_E_INVALID, "bad shard: row_offset %d row_stride %d height %d", p->row_offset,
                 p->row_stride, p->height);
   if ((long long)p->width * p->height >= (1LL << 32))
-    return fail(RT_E_INVALID, "image too large for 32-bit pixel ids");
-  if (p->flags & ~RT_FLAG_NO_CULL) return fail(RT_E_INVALID, "unknown flags 0x%x", p->flags);
+    return set_error(RT_E_INVALID, "image too large for 32-bit pixel ids");
+  if (p->flags & ~RT_FLAG_NO_CULL) return set_error(RT_E_INVALID, "unknown flags 0x%x", p->flags);
   return RT_OK;
 }
 
 int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigned char* d_rgb8,
                      void* stream_) {
-  if (!c) return fail(RT_E_INVALID, "rt_render_device: ctx is NULL");
+  if (!c) return set_error(RT_E_INVALID, "rt_render_device: ctx is NULL");
   int rc = check_params(p);
   if (rc) return rc;
-  if (c->n < 0) return fail(RT_E_SCENE, "rt_render_device: no scene set");
+  if (c->n < 0) return set_error(RT_E_SCENE, "rt_render_device: no scene set");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = stream_ ? (hipStream_t)stream_ : c->stream;
   const int rows = rt_rows_owned(p->height, p->row_offset, p->row_stride);
@@ -327,7 +334,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   if (s_chunk < 1) s_chunk = 1;
   if (s_chunk > (size_t)p->spp) s_chunk = p->spp;
   while (s_chunk > 1 && P * s_chunk >= (1ULL << 32)) s_chunk /= 2;
-  if (P * s_chunk >= (1ULL << 32)) return fail(RT_E_INVALID, "shard too large");
+  if (P * s_chunk >= (1ULL << 32)) return set_error(RT_E_INVALID, "shard too large");
   const int nchunks = (int)((p->spp + s_chunk - 1) / s_chunk);
   rc = ensure_buf(&c->d_samples, &c->samples_cap, s_chunk * P * 3);
   if (rc) return rc;
@@ -420,7 +427,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
 }
 
 int rt_context_sync_stats(rt_context* c, rt_stats* s) {
-  if (!c) return fail(RT_E_INVALID, "rt_context_sync_stats: ctx is NULL");
+  if (!c) return set_error(RT_E_INVALID, "rt_context_sync_stats: ctx is NULL");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipEventSynchronize(c->ev_all1));
   unsigned long long cnt[3] = {0, 0, 0};
@@ -462,7 +469,7 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
 int rt_quantize_device(rt_context* c, const double* d_accum, int width, int rows, int spp,
                        unsigned char* d_rgb8, void* stream_) {
   if (!c || !d_accum || !d_rgb8 || width <= 0 || rows < 0 || spp <= 0)
-    return fail(RT_E_INVALID, "rt_quantize_device: bad arguments");
+    return set_error(RT_E_INVALID, "rt_quantize_device: bad arguments");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = stream_ ? (hipStream_t)stream_ : c->stream;
   const size_t n = (size_t)width * rows * 3;
@@ -476,7 +483,7 @@ int rt_quantize_device(rt_context* c, const double* d_accum, int width, int rows
 static int get_default_context(rt_context** out) {
   std::lock_guard<std::mutex> lk(g_default_mu);
   int dev = default_device();
-  if (dev < 0 || dev >= 64) return fail(RT_E_INVALID, "RT_DEVICE out of range");
+  if (dev < 0 || dev >= 64) return set_error(RT_E_INVALID, "RT_DEVICE out of range");
   if (!g_default[dev]) {
     int rc = rt_context_create(dev, &g_default[dev]);
     if (rc) return rc;
@@ -488,7 +495,7 @@ static int get_default_context(rt_context** out) {
 int rt_render(const rt_sphere* sph, int n, const rt_camera* cam, const rt_params* p,
               double* accum_rgb, unsigned char* rgb8, rt_stats* stats) {
   if (!cam || !p || (!accum_rgb && !rgb8) || n < 0 || (n > 0 && !sph))
-    return fail(RT_E_INVALID, "rt_render: bad arguments");
+    return set_error(RT_E_INVALID, "rt_render: bad arguments");
   int rc = check_params(p);
   if (rc) return rc;
   rt_context* c = nullptr;
@@ -514,7 +521,7 @@ int rt_render(const rt_sphere* sph, int n, const rt_camera* cam, const rt_params
 
 // Debug entry: run one f64 primitive on the device (numerics parity tests).
 int rt_debug_probe_f64(int op, const double* x, const double* y, double* out, int n) {
-  if (!x || !y || !out || n < 0) return fail(RT_E_INVALID, "rt_debug_probe_f64: bad arguments");
+  if (!x || !y || !out || n < 0) return set_error(RT_E_INVALID, "rt_debug_probe_f64: bad arguments");
   if (n == 0) return RT_OK;
   rt_context* c = nullptr;
   int rc = get_default_context(&c);
@@ -541,7 +548,7 @@ int rt_debug_probe_f64(int op, const double* x, const double* y, double* out, in
 int rt_debug_world_hit(const rt_sphere* sph, int n, const double* rays, int count, double* out,
                        int cull) {
   if (!rays || !out || count < 0 || n < 0 || (n > 0 && !sph))
-    return fail(RT_E_INVALID, "rt_debug_world_hit: bad arguments");
+    return set_error(RT_E_INVALID, "rt_debug_world_hit: bad arguments");
   if (count == 0) return RT_OK;
   rt_context* c = nullptr;
   int rc = get_default_context(&c);

@@ -6,6 +6,8 @@ Mirrors the reference's pieces by name and meaning:
 * ``camera_look_at(...)``         look-at pinhole extension for the final scene
 * ``scene_two_spheres()``         main.cc:61-63 world
 * ``scene_random_spheres(seed)``  final random-spheres world
+* ``load_scene / parse_scene``    scene/camera files (DESIGN.md §Scene files)
+* ``save_scene / format_scene``   ... and back (bit-exact round trip)
 * ``render(...)``                 the main.cc:72-88 pixel loop for a shard of rows
 * ``write_ppm(...)``              main.cc:70 header + color.h:21-23 pixel lines
 
@@ -15,6 +17,7 @@ cameras are ``(4, 3)`` float64 arrays (origin, lower_left, horizontal, vertical)
 from __future__ import annotations
 
 import ctypes as C
+from dataclasses import dataclass
 from typing import Optional
 
 import numpy as np
@@ -84,6 +87,60 @@ def scene_random_spheres(seed: int = 1) -> np.ndarray:
     buf = (RtSphere * n)()
     L.rt_scene_random_spheres(seed, buf, n)
     return np.frombuffer(buf, dtype=np.float64, count=4 * n).reshape(n, 4).copy()
+
+
+@dataclass
+class SceneFile:
+    """A parsed scene file: spheres (n, 4), camera (4, 3) and the pixel-loop
+    parameters (0 / 50 / 0 where the file's ``render`` line is silent)."""
+    spheres: np.ndarray
+    camera: np.ndarray
+    width: int = 0
+    height: int = 0
+    spp: int = 0
+    max_depth: int = 50
+    seed: int = 0
+
+
+def _scene_call(fn, arg) -> SceneFile:
+    L = _lib.load()
+    cam = RtCamera()
+    p = params(0, 0, 0)
+    n = getattr(L, fn)(arg, None, 0, C.byref(cam), C.byref(p))
+    check(min(n, 0), fn)
+    buf = (RtSphere * max(1, n))()
+    check(min(getattr(L, fn)(arg, buf, n, None, None), 0), fn)
+    arr = np.frombuffer(buf, dtype=np.float64, count=4 * n).reshape(n, 4).copy()
+    return SceneFile(arr, _camera_array(cam), p.width, p.height, p.spp, p.max_depth, p.seed)
+
+
+def parse_scene(text: str) -> SceneFile:
+    """rt_scene_parse over the text of a ``psrt-scene 1`` file."""
+    return _scene_call("rt_scene_parse", text.encode())
+
+
+def load_scene(path: str) -> SceneFile:
+    """rt_scene_load: read a ``psrt-scene 1`` file."""
+    return _scene_call("rt_scene_load", str(path).encode())
+
+
+def format_scene(spheres, camera=None, width: Optional[int] = None, height: int = 0,
+                 spp: int = 0, max_depth: int = 50, seed: int = 0) -> str:
+    """rt_scene_format: the file text (``render`` line only when width is given)."""
+    L = _lib.load()
+    buf, n = _spheres(spheres)
+    cam = C.byref(_camera(camera)) if camera is not None else None
+    p = C.byref(params(width, height, spp, max_depth, seed)) if width is not None else None
+    size = L.rt_scene_format(buf, n, cam, p, None, 0)
+    check(int(min(size, 0)), "rt_scene_format")
+    out = C.create_string_buffer(int(size) + 1)
+    L.rt_scene_format(buf, n, cam, p, out, size + 1)
+    return out.value.decode()
+
+
+def save_scene(path: str, spheres, camera=None, **render_args) -> None:
+    with open(path, "w") as f:
+        f.write(format_scene(spheres, camera, **render_args))
 
 
 def stats_dict(s: RtStats) -> dict:
