@@ -286,6 +286,7 @@ static psrt::BvhView bvh_view(const rt_context* c) {
   v.big_idx = c->d_big;
   v.n_nodes = c->n_nodes;
   v.n_big = c->n_big;
+  v.n_leaf = c->n_leaf;
   v.r_check = c->r_check;
   v.cell_start = c->d_cell_start;
   v.cell_items = c->d_cell_items;
@@ -391,6 +392,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     const double* ir = c->d_inv_r;
     const dim3 blk(psrt::kTraceBlock);
     const bool lds = c->n_nodes + 1 <= psrt::kLdsNodes && c->n <= psrt::kLdsSpheres &&
+                     c->n_leaf <= psrt::kLdsSpheres &&
                      !std::getenv("PSRT_NO_LDS");
     auto launch = [&](auto kern, int grid) {
       hipLaunchKernelGGL(kern, dim3(grid), blk, 0, st, g4, ir, c->d_samples, ta, bv);

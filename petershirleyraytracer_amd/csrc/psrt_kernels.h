@@ -32,7 +32,7 @@ struct BvhView {
   const double4* __restrict__ leaf_geo;  // sphere per leaf slot
   const int* __restrict__ leaf_idx;      // original index per leaf slot
   const int* __restrict__ big_idx;       // spheres tested on every ray
-  int n_nodes, n_big;
+  int n_nodes, n_big, n_leaf;
   double r_check;
   // point-location grid (psrt_bvh.h GridHost)
   const int* __restrict__ cell_start;

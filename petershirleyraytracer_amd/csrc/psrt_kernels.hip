@@ -324,11 +324,13 @@ __device__ __forceinline__ double root_box_entry(const BvhView& bv, double ox, d
 
 // The BVH walk (stackless, skip links) for a bounded ray, continuing from the
 // (bt, bi) hit_quick left.
-template <bool kDiag>
+template <bool kDiag, bool kLdsLeaves>
 __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __restrict__ nodes,
-                                             int hint, double ox, double oy,
-                                             double oz, double dx, double dy, double dz,
-                                             double A, double& bt, int& bi, CullStats& cs) {
+                                             const int* __restrict__ leaf_idx,
+                                             const double4* __restrict__ lgeo, int hint,
+                                             double ox, double oy, double oz, double dx, double dy,
+                                             double dz, double A, double& bt, int& bi,
+                                             CullStats& cs) {
   // Far origins are re-based at their root-box entry o' = o + t0 d (FP64), so
   // the FP32 slab test sees |o'| <= the scene scale and its error bound holds;
   // box intervals are then tested over [-t0, bt - t0]. The exact sphere tests
@@ -345,9 +347,9 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
   int node = 0;
   if constexpr (kDiag) ++cs.trav_rays;
   // Two nodes per trip: in DFS skip-link order an interior hit always
-  // continues at node+1, so node+1 is loaded and box-tested alongside node
-  // (independent work that overlaps the node-load latency); the trip then
-  // advances two levels when node is an interior hit. Node n_nodes is a padding
+  // continues at node+1, so node+1 is loaded alongside node and, when node is
+  // an interior hit, box-tested in the same trip; the trip then advances two
+  // levels. Node n_nodes is a padding
   // node (psrt_bvh.cpp), so node+1 is always readable.
   while (node < bv.n_nodes) {
     if constexpr (kDiag) {
@@ -356,10 +358,10 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
     const float4 a0 = nodes[2 * node], a1 = nodes[2 * node + 1];
     const float4 b0 = nodes[2 * node + 2], b1 = nodes[2 * node + 3];
     // slab distances; FP32 FMA is fine here: the test only needs to be
-    // conservative, and the box padding covers its rounding (psrt_bvh.cpp)
+    // conservative, and the box padding covers its rounding (psrt_bvh.cpp).
+    // node+1's test runs only where node is an interior hit: the walk is
+    // VALU-issue bound, so skipping it beats overlapping it (measured).
     const bool hit_a = slab_hit(a0, a1, ix, iy, iz, oix, oiy, oiz, tlo, tmax);
-    const bool hit_b = slab_hit(b0, b1, ix, iy, iz, oix, oiy, oiz, tlo, tmax);
-    cs.boxes += 2;
     const int leaf_a = __float_as_int(a1.w), leaf_b = __float_as_int(b1.w);
     int next, leaf = -1;
     if (!hit_a) {
@@ -367,7 +369,7 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
     } else if (leaf_a >= 0) {
       leaf = leaf_a;
       next = __float_as_int(a0.w);
-    } else if (!hit_b) {
+    } else if (!slab_hit(b0, b1, ix, iy, iz, oix, oiy, oiz, tlo, tmax)) {
       next = __float_as_int(b0.w);
     } else if (leaf_b >= 0) {
       leaf = leaf_b;
@@ -375,6 +377,7 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
     } else {
       next = node + 2;
     }
+    cs.boxes += 2;
     if (leaf >= 0) {
       const int first = leaf >> 8, cnt = leaf & 255;
       if constexpr (kDiag) {
@@ -382,9 +385,10 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
         if (first_active_lane()) ++cs.wave_leaf_trips;
       }
       for (int k = first; k < first + cnt; ++k) {
-        const int idx = bv.leaf_idx[k];
+        const int idx = leaf_idx[k];
         if (idx == hint) continue;
-        test_sphere(bv.leaf_geo[k], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
+        test_sphere(kLdsLeaves ? lgeo[idx] : bv.leaf_geo[k], idx, ox, oy, oz, dx, dy, dz, A, bt,
+                    bi);
         ++cs.spheres;
       }
       tmax = tmax_up(bt - t0);
@@ -402,10 +406,15 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
   int bi;
   SectionClock<false> noclk;
   if (!hit_quick(geo, geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs, noclk))
-    hit_traverse<false>(bv, bv.nodes, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs);
+    hit_traverse<false, false>(bv, bv.nodes, bv.leaf_idx, geo, hint, ox, oy, oz, dx, dy, dz, A,
+                               bt, bi, cs);
   best_t = bt;
   return bi;
 }
+
+#ifndef PSRT_LDS_LEAVES
+#define PSRT_LDS_LEAVES 1  // leaf index + sphere reads from LDS in the walk
+#endif
 
 #ifndef PSRT_TRACE_WAVES
 #define PSRT_TRACE_WAVES 6  // min waves per SIMD requested from the register allocator
@@ -427,14 +436,17 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   __shared__ float4 s_nodes[kLds ? 2 * kLdsNodes : 1];
   __shared__ double4 s_geo[kLds ? kLdsSpheres : 1];
   __shared__ double s_inv[kLds ? kLdsSpheres : 1];
-  if constexpr (kLds) {  // host guarantees n_nodes <= kLdsNodes and n <= kLdsSpheres
+  __shared__ int s_leaf[kLds ? kLdsSpheres : 1];
+  if constexpr (kLds) {  // host guarantees n_nodes < kLdsNodes and n <= kLdsSpheres
     for (int e = threadIdx.x; e < 2 * (bv.n_nodes + 1); e += blockDim.x) s_nodes[e] = bv.nodes[e];
     for (int e = threadIdx.x; e < a.n; e += blockDim.x) s_geo[e] = geo[e], s_inv[e] = inv_r[e];
+    for (int e = threadIdx.x; e < bv.n_leaf; e += blockDim.x) s_leaf[e] = bv.leaf_idx[e];
     __syncthreads();
   }
   const float4* __restrict__ nodes = kLds ? s_nodes : bv.nodes;
   const double4* __restrict__ lgeo = kLds ? s_geo : geo;
   const double* __restrict__ linv = kLds ? s_inv : inv_r;
+  const int* __restrict__ lleaf = (kLds && PSRT_LDS_LEAVES) ? s_leaf : bv.leaf_idx;
 
   // wave-uniform work window
   uint64_t win_base = 0;
@@ -539,7 +551,8 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       const uint64_t movable = __ballot(active && !pending);
       if (pend != 0 && ((unsigned)__popcll(pend) >= a.batch || movable == 0)) {
         if (pending) {
-          hit_traverse<kStamps>(bv, nodes, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi, cs);
+          hit_traverse<kStamps, kLds && PSRT_LDS_LEAVES>(bv, nodes, lleaf, lgeo, hint, ox, oy,
+                                                         oz, dx, dy, dz, A, pbt, pbi, cs);
           pending = false;
           resolved = true;
         }
