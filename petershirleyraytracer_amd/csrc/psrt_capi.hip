@@ -376,6 +376,9 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     const char* f = std::getenv("PSRT_RNG_FILL");  // tuning knob (default 2)
     ta.rng_fill = f ? std::atoi(f) : 2;
     if (ta.rng_fill < 0) ta.rng_fill = 0;
+    const char* r = std::getenv("PSRT_REFILL_MIN");  // tuning knob (default 8 of 64 lanes)
+    ta.refill_min = r ? (unsigned)std::atoi(r) : 8u;
+    if (ta.refill_min < 1) ta.refill_min = 1;
   }
   const bool use_bvh = c->bvh && !(p->flags & RT_FLAG_NO_CULL);
   const psrt::BvhView bv = bvh_view(c);

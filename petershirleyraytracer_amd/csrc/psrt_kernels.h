@@ -25,6 +25,7 @@ struct TraceArgs {
   unsigned long long* stamps;       // diagnostic build: cycles per section (kSecCount)
   unsigned batch;                   // parked lanes that trigger a batched BVH pass
   int rng_fill;                     // look-ahead trials per lane per iteration (min)
+  unsigned refill_min;              // idle lanes that trigger the finish + refill block
 };
 
 struct BvhView {

@@ -454,6 +454,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   bool exhausted = false;
 
   bool active = false;
+  bool done = false;  // sample finished; its colour is stored by the next refill block
   double ox = 0, oy = 0, oz = 0, dx = 0, dy = 0, dz = 0, A = 0;
   int k = 0;          // bounces (hits) so far: current trace is at depth max_depth-k
   uint64_t rng = 0;
@@ -473,10 +474,34 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   clk.start();
 
   for (;;) {
-    // ---- refill lanes whose sample finished (wavefront ballot compaction) ----
+    // ---- finish + refill lanes whose sample ended (wavefront ballot compaction) ----
+    // The block runs for the wave once at least refill_min lanes are idle (or
+    // none is live): its cost is per wave, so batching finished lanes pays
+    // for the few iterations they sit idle.
     const bool need = !active;
     const uint64_t need_mask = __ballot(need);
-    if (need_mask != 0 && !exhausted) {
+    const bool run_block = need_mask != 0 && ((unsigned)__popcll(need_mask) >= a.refill_min ||
+                                              need_mask == __ballot(1));
+    if (run_block) {
+      // sky (main.cc:46-48) x 0.5^k, or black; store
+      if (done) {
+        double col_r = 0.0, col_g = 0.0, col_b = 0.0;
+        if (pbi < 0 && a.max_depth >= 0) {
+          const double y = (1.0 / __builtin_sqrt(A)) * dy;
+          const double tt = 0.5 * (y + 1.0);
+          const double w = 1.0 - tt;
+          col_r = half_pow(w + tt * 0.5, k);
+          col_g = half_pow(w + tt * 0.7, k);
+          col_b = half_pow(w + tt * 1.0, k);
+        }
+        double* dst = samples + ((size_t)sl * a.pixels + q) * 3;
+        dst[0] = col_r;
+        dst[1] = col_g;
+        dst[2] = col_b;
+        done = false;
+      }
+    }
+    if (run_block && !exhausted) {
       const unsigned cnt = (unsigned)__popcll(need_mask);
       const unsigned rank = mbcnt64(need_mask);
       uint64_t nb = 0;
@@ -528,7 +553,6 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     // lanes wait (or nothing else can progress): the pass then runs at high
     // SIMD occupancy instead of once per iteration for a handful of lanes.
     bool resolved = false, finish = false;
-    double col_r = 0.0, col_g = 0.0, col_b = 0.0;
     if (active && !pending) {
       if (a.max_depth < 0) {  // main.cc:36-37 at the first call: black, no trace
         finish = true;
@@ -612,20 +636,9 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     }
     clk.mark(kSecScatter);
 
-    // ---- sample done: sky (main.cc:46-48) x 0.5^k, or black; store ----
+    // ---- sample done: colour and store in the next finish + refill block ----
     if (finish) {
-      if (hit < 0 && a.max_depth >= 0) {
-        const double y = (1.0 / __builtin_sqrt(A)) * dy;
-        const double tt = 0.5 * (y + 1.0);
-        const double w = 1.0 - tt;
-        col_r = half_pow(w + tt * 0.5, k);
-        col_g = half_pow(w + tt * 0.7, k);
-        col_b = half_pow(w + tt * 1.0, k);
-      }
-      double* dst = samples + ((size_t)sl * a.pixels + q) * 3;
-      dst[0] = col_r;
-      dst[1] = col_g;
-      dst[2] = col_b;
+      done = true;
       active = false;
     }
     clk.mark(kSecFillShade);

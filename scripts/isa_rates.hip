@@ -1,0 +1,121 @@
+// isa_rates.hip — diagnostic microbenchmark: issue cost of the VALU
+// instruction classes the trace kernel is made of (FP64 add/mul/fma, the f64
+// division/sqrt helpers, FP32, 32-bit integer multiply, 64-bit mad), on
+// gfx950. Each kernel runs 8 independent chains of one instruction per lane,
+// so the figure is throughput, not latency. Reported: cycles per
+// wave-instruction on one SIMD, with 1 and with 8 waves per SIMD.
+//
+//   hipcc --offload-arch=gfx950 -O3 scripts/isa_rates.hip -o /tmp/isa_rates
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CHAINS 8
+#define UNROLL 16
+#define ITERS 256
+
+template <int kOp>
+__global__ void __launch_bounds__(512) bench(unsigned long long* cyc, double* sink) {
+  double d[CHAINS];
+  float f[CHAINS];
+  unsigned u[CHAINS];
+  unsigned long long w[CHAINS];
+  for (int c = 0; c < CHAINS; ++c) {
+    d[c] = 1.0 + threadIdx.x * 1e-9 + c;
+    f[c] = 1.0f + threadIdx.x * 1e-6f + c;
+    u[c] = threadIdx.x * 2654435761u + c;
+    w[c] = (unsigned long long)threadIdx.x * 0x9E3779B97F4A7C15ULL + c;
+  }
+  const double dy = 1.0000001;
+  const float fy = 1.0000001f;
+  const unsigned uy = 0x4C957F2Du;
+  unsigned long long t0;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) {
+#pragma unroll
+      for (int c = 0; c < CHAINS; ++c) {
+        if constexpr (kOp == 0) asm volatile("v_add_f64 %0, %0, %1" : "+v"(d[c]) : "v"(dy));
+        if constexpr (kOp == 1) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(d[c]) : "v"(dy));
+        if constexpr (kOp == 2) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(d[c]) : "v"(dy));
+        if constexpr (kOp == 3) asm volatile("v_add_f32 %0, %0, %1" : "+v"(f[c]) : "v"(fy));
+        if constexpr (kOp == 4) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(f[c]) : "v"(fy));
+        if constexpr (kOp == 5) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(u[c]) : "v"(uy));
+        if constexpr (kOp == 6)
+          asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(w[c]) : "v"(u[c]), "v"(uy) : "vcc");
+        if constexpr (kOp == 7) asm volatile("v_rcp_f64 %0, %0" : "+v"(d[c]));
+        if constexpr (kOp == 8) asm volatile("v_rsq_f64 %0, %0" : "+v"(d[c]));
+        if constexpr (kOp == 9) asm volatile("v_cvt_f64_i32 %0, %1" : "=v"(d[c]) : "v"(u[c]));
+        if constexpr (kOp == 10) asm volatile("v_ldexp_f64 %0, %0, %1" : "+v"(d[c]) : "v"(u[c]));
+        if constexpr (kOp == 11) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(u[c]) : "v"(uy));
+        if constexpr (kOp == 12) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(u[c]) : "v"(uy));
+        if constexpr (kOp == 13) asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(w[c]) : "v"(w[0]));
+        if constexpr (kOp == 14) asm volatile("v_div_fixup_f64 %0, %0, %1, %1" : "+v"(d[c]) : "v"(dy));
+        if constexpr (kOp == 15) asm volatile("v_cmp_gt_f64 vcc, %0, %1" ::"v"(d[c]), "v"(dy) : "vcc");
+        if constexpr (kOp == 16) asm volatile("v_cvt_f32_f64 %0, %1" : "=v"(f[c]) : "v"(d[c]));
+        if constexpr (kOp == 17) asm volatile("v_min_f64 %0, %0, %1" : "+v"(d[c]) : "v"(dy));
+        if constexpr (kOp == 18) asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(w[c]) : "v"(w[0]));
+      }
+    }
+  }
+  unsigned long long t1;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+  double acc = 0;
+  for (int c = 0; c < CHAINS; ++c) acc += d[c] + f[c] + u[c] + (double)w[c];
+  sink[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+  if (threadIdx.x % 64 == 0) atomicMax(cyc, t1 - t0);
+}
+
+static const char* kNames[] = {"v_add_f64",    "v_mul_f64",     "v_fma_f64",     "v_add_f32",
+                               "v_fma_f32",    "v_mul_lo_u32",  "v_mad_u64_u32", "v_rcp_f64",
+                               "v_rsq_f64",    "v_cvt_f64_i32", "v_ldexp_f64",   "v_xor_b32",
+                               "v_mul_hi_u32", "v_pk_fma_f32",  "v_div_fixup_f64", "v_cmp_gt_f64",
+                               "v_cvt_f32_f64", "v_min_f64",    "v_lshl_add_u64"};
+
+template <int kOp>
+void run(int cus, double* sink, unsigned long long* dcyc) {
+  const double n = (double)ITERS * UNROLL * CHAINS;
+  double res[2];
+  const int waves[2] = {1, 8};
+  for (int m = 0; m < 2; ++m) {
+    // waves per SIMD x 4 SIMDs per CU; one 256-thread block = 1 wave per SIMD
+    const int blocks = cus * waves[m];
+    (void)hipMemset(dcyc, 0, sizeof *dcyc);
+    hipLaunchKernelGGL(bench<kOp>, dim3(blocks), dim3(256), 0, 0, dcyc, sink);
+    (void)hipDeviceSynchronize();
+    unsigned long long c = 0;
+    (void)hipMemcpy(&c, dcyc, sizeof c, hipMemcpyDeviceToHost);
+    // max over waves of its loop cycles; with w waves sharing a SIMD the SIMD
+    // issued w * n instructions in that time
+    res[m] = (double)c / (n * waves[m]);
+  }
+  std::printf("{\"insn\": \"%s\", \"cyc_per_wave_insn_1w\": %.3f, \"cyc_per_simd_insn_8w\": %.3f}\n",
+              kNames[kOp], res[0], res[1]);
+}
+
+template <int... kOps>
+void run_all(int cus, double* sink, unsigned long long* dcyc) {
+  (run<kOps>(cus, sink, dcyc), ...);
+}
+
+int main() {
+  int dev = 0;
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, dev) != hipSuccess) {
+    std::fprintf(stderr, "no device\n");
+    return 1;
+  }
+  const int cus = p.multiProcessorCount;
+  double* sink = nullptr;
+  unsigned long long* dcyc = nullptr;
+  if (hipMalloc(&sink, sizeof(double) * cus * 8 * 256) != hipSuccess ||
+      hipMalloc(&dcyc, sizeof(unsigned long long)) != hipSuccess)
+    return 1;
+  run<0>(cus, sink, dcyc);  // warm-up (clocks)
+  run_all<0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18>(cus, sink, dcyc);
+  (void)hipFree(sink);
+  (void)hipFree(dcyc);
+  return 0;
+}
