@@ -370,8 +370,8 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   const bool stamps = std::getenv("PSRT_STAMPS") != nullptr;  // diagnostic build
   ta.stamps = c->d_counters + 8;
   {
-    const char* e = std::getenv("PSRT_BATCH");  // tuning knob (default 24 of 64 lanes)
-    ta.batch = e ? (unsigned)std::atoi(e) : 24u;
+    const char* e = std::getenv("PSRT_BATCH");  // tuning knob (default 18 of 64 lanes)
+    ta.batch = e ? (unsigned)std::atoi(e) : 18u;
     if (ta.batch < 1) ta.batch = 1;
     const char* f = std::getenv("PSRT_RNG_FILL");  // tuning knob (default 2)
     ta.rng_fill = f ? std::atoi(f) : 2;

@@ -437,12 +437,20 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   __shared__ double4 s_geo[kLds ? kLdsSpheres : 1];
   __shared__ double s_inv[kLds ? kLdsSpheres : 1];
   __shared__ int s_leaf[kLds ? kLdsSpheres : 1];
+  // camera basis (only the refill block reads it): from LDS rather than held
+  // in 24 SGPRs across the loop, which spills them into VGPR lanes
+  __shared__ double s_cam[12];
+  if (threadIdx.x < 12)
+    s_cam[threadIdx.x] = threadIdx.x < 3   ? a.org[threadIdx.x]
+                         : threadIdx.x < 6 ? a.llc[threadIdx.x - 3]
+                         : threadIdx.x < 9 ? a.hor[threadIdx.x - 6]
+                                           : a.ver[threadIdx.x - 9];
   if constexpr (kLds) {  // host guarantees n_nodes < kLdsNodes and n <= kLdsSpheres
     for (int e = threadIdx.x; e < 2 * (bv.n_nodes + 1); e += blockDim.x) s_nodes[e] = bv.nodes[e];
     for (int e = threadIdx.x; e < a.n; e += blockDim.x) s_geo[e] = geo[e], s_inv[e] = inv_r[e];
     for (int e = threadIdx.x; e < bv.n_leaf; e += blockDim.x) s_leaf[e] = bv.leaf_idx[e];
-    __syncthreads();
   }
+  __syncthreads();
   const float4* __restrict__ nodes = kLds ? s_nodes : bv.nodes;
   const double4* __restrict__ lgeo = kLds ? s_geo : geo;
   const double* __restrict__ linv = kLds ? s_inv : inv_r;
@@ -524,10 +532,11 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
           // main.cc:80-81, camera.h:25-28
           const double u = ((double)i + random_double(rng)) / (double)(a.width - 1);
           const double v = ((double)j + random_double(rng)) / (double)(a.height - 1);
-          ox = a.org[0], oy = a.org[1], oz = a.org[2];
-          dx = ((a.llc[0] + u * a.hor[0]) + v * a.ver[0]) - ox;
-          dy = ((a.llc[1] + u * a.hor[1]) + v * a.ver[1]) - oy;
-          dz = ((a.llc[2] + u * a.hor[2]) + v * a.ver[2]) - oz;
+          const double* cam = s_cam;  // origin, lower_left, horizontal, vertical
+          ox = cam[0], oy = cam[1], oz = cam[2];
+          dx = ((cam[3] + u * cam[6]) + v * cam[9]) - ox;
+          dy = ((cam[4] + u * cam[7]) + v * cam[10]) - oy;
+          dz = ((cam[5] + u * cam[8]) + v * cam[11]) - oz;
           A = (dx * dx + dy * dy) + dz * dz;
           k = 0;
           hint = -1;
