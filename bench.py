@@ -72,6 +72,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--save-ppm", default="")
     ap.add_argument("--no-cull", action="store_true", help="force the linear sphere sweep")
+    ap.add_argument("--no-fixpoint", action="store_true",
+                    help="trace provably trapped paths to max_depth (DESIGN.md §9)")
     return ap.parse_args()
 
 
@@ -172,7 +174,7 @@ def main():
 
     import petershirleyraytracer_amd as P
     from petershirleyraytracer_amd.dist import gather_frame, rows_owned, shard
-    from petershirleyraytracer_amd.render import FLAG_NO_CULL
+    from petershirleyraytracer_amd.render import FLAG_NO_CULL, FLAG_NO_FIXPOINT
 
     torch.cuda.set_device(local)
     distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ or "MASTER_PORT" in os.environ
@@ -186,7 +188,8 @@ def main():
     off, stride = shard(rank, world)
     rows = rows_owned(h, rank, world)
     prm = P.params(w, h, spp, args.max_depth, args.seed, off, stride,
-                   FLAG_NO_CULL if args.no_cull else 0)
+                   (FLAG_NO_CULL if args.no_cull else 0)
+                   | (FLAG_NO_FIXPOINT if args.no_fixpoint else 0))
     dev = torch.device("cuda", local)
     acc = torch.zeros((rows, w, 3), dtype=torch.float64, device=dev)
     rgb = torch.zeros((h, w, 3), dtype=torch.uint8, device=dev) if rank == 0 else None

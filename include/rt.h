@@ -74,6 +74,7 @@ typedef struct {
 /* flags */
 #define RT_FLAG_NONE 0
 #define RT_FLAG_NO_CULL 1u /* force the linear sphere sweep (no BVH): same bits, slower */
+#define RT_FLAG_NO_FIXPOINT 2u /* trace provably trapped paths to max_depth: same bits, slower */
 
 typedef struct {
   int width;      /* image_width  (main.cc:57)                              */

@@ -315,7 +315,7 @@ static int check_params(const rt_params* p) {
                 p->row_stride, p->height);
   if ((long long)p->width * p->height >= (1LL << 32))
     return set_error(RT_E_INVALID, "image too large for 32-bit pixel ids");
-  if (p->flags & ~RT_FLAG_NO_CULL) return set_error(RT_E_INVALID, "unknown flags 0x%x", p->flags);
+  if (p->flags & ~(RT_FLAG_NO_CULL | RT_FLAG_NO_FIXPOINT)) return set_error(RT_E_INVALID, "unknown flags 0x%x", p->flags);
   return RT_OK;
 }
 
@@ -381,7 +381,8 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     if (ta.refill_min < 1) ta.refill_min = 1;
   }
   const bool use_bvh = c->bvh && !(p->flags & RT_FLAG_NO_CULL);
-  const psrt::BvhView bv = bvh_view(c);
+  psrt::BvhView bv = bvh_view(c);
+  bv.fixpoint = !(p->flags & RT_FLAG_NO_FIXPOINT) && !std::getenv("PSRT_NO_FIXPOINT");
   HIP_TRY(hipEventRecord(c->ev_all0, st));
   for (int ch = 0; ch < nchunks; ++ch) {
     const int s0 = (int)(ch * s_chunk);

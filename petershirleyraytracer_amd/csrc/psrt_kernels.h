@@ -40,6 +40,7 @@ struct BvhView {
   const int* __restrict__ cell_items;
   float glo[3], ghi[3], ginv, gmargin;  // FP32 copies (conservative use only)
   int gdims[3];
+  int fixpoint;  // end provably trapped paths early (hit_quick; RT_FLAG_NO_FIXPOINT clears it)
 };
 
 struct ReduceArgs {

@@ -151,29 +151,34 @@ __device__ __forceinline__ HitRec hit_record_of(const double4 s, double ir, doub
 // best_t by >= 2^-5 D; that gap exceeds the root error whenever
 // D >= 2^-17 |amc|, guaranteed by C^2 >= 2^-33 (C + r^2)(C + 2 r^2). Origins
 // nearer the surface always take the full test.
-__device__ __forceinline__ void test_sphere(const double4 s, int idx, double ox, double oy,
+// Returns false when the pre-reject decided the sphere, true when the full
+// test ran. *c_out (if given) receives C = amc.amc - r^2 as sphere.cc:11 forms it.
+__device__ __forceinline__ bool test_sphere(const double4 s, int idx, double ox, double oy,
                                             double oz, double dx, double dy, double dz,
-                                            double A, double& best_t, int& best_i) {
+                                            double A, double& best_t, int& best_i,
+                                            double* c_out = nullptr) {
   const double ax = ox - s.x, ay = oy - s.y, az = oz - s.z;
   const double c = ((ax * ax + ay * ay) + az * az) - s.w;
+  if (c_out) *c_out = c;
   if (c > 0.0 && best_t < 1e100) {
     const double c2 = c * c, k2 = 2.0 * (c + 2.0 * s.w);
     if (c2 >= 0x1p-34 * (c + s.w) * k2 && (best_t * best_t) * A * k2 * (1.0 + 0x1p-4) < c2)
-      return;
+      return false;
   }
   const double hb = (dx * ax + dy * ay) + dz * az;
   const double disc = hb * hb - A * c;
-  if (disc < 0.0) return;
+  if (disc < 0.0) return true;
   const double sq = __builtin_sqrt(disc);
   double t = (-hb - sq) / A;
   if (t < 0.0 || t > best_t) {
     t = (-hb + sq) / A;
-    if (t < 0.0 || t > best_t) return;
+    if (t < 0.0 || t > best_t) return true;
   }
   if (t < best_t || idx > best_i) {  // equal t: the later index wins
     best_t = t;
     best_i = idx;
   }
+  return true;
 }
 
 // Point query for a short segment [o, o + bt*d] (the common case: the ray
@@ -184,7 +189,7 @@ __device__ __forceinline__ int grid_point_query(const double4* __restrict__ lgeo
                                                 const BvhView& bv, int hint, double ox,
                                                 double oy, double oz, double dx, double dy,
                                                 double dz, double A, double& bt, int& bi,
-                                                unsigned& tests) {
+                                                unsigned& tests, bool& full) {
   if (!(bt < 1e30)) return 0;
   // FP32 is enough: the test is conservative and its error (~2^-22 of the
   // scene scale) is far inside the margin (pad/4, psrt_bvh.cpp)
@@ -211,7 +216,7 @@ __device__ __forceinline__ int grid_point_query(const double4* __restrict__ lgeo
   for (int e = e0; e < e1; ++e) {
     const int idx = bv.cell_items[e];
     if (idx == hint) continue;
-    test_sphere(lgeo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
+    full |= test_sphere(lgeo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
     ++tests;
   }
   return 1;
@@ -258,14 +263,29 @@ __device__ __forceinline__ double root_box_entry(const BvhView& bv, double ox, d
                                                  double oz, double dx, double dy, double dz,
                                                  double tmax);
 
+// Trapped-path termination. Let the ray start at o on sphere j
+// (the previous hit, `hint`) with C_j(o) = ((ax*ax + ay*ay) + az*az) - r*r
+// computed as exactly 0. Then for EVERY direction d: A*C = +0, disc = fl(hb*hb),
+// sqrt(fl(hb*hb)) = |hb| (binary64, no under/overflow), so sphere j's accepted
+// root is t = +-0 and p = o + t*d equals o in value: the path never leaves o.
+// If, besides, every other candidate sphere was decided without the full test
+// (pre-rejected: origin outside, clear of the surface; or outside the grid
+// cell / grid), each of those has no root <= 0 in any direction, so every
+// later world.hit returns sphere j at t = +-0 again, whatever the draws. The
+// path then hits until depth runs out: main.cc:36-37 returns black. The
+// guards keep hb far from under/overflow for every reachable direction
+// d = ((p + n) + rv) - p (n = +-(o - c)/r, rv in n's hemisphere, so
+// |hb| >= r/2): 2^-700 <= r^2 <= 2^700 and |o|_inf <= 2^40.
 template <class Clock>
 __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
                                           const double4* __restrict__ lgeo, int n,
                                           const BvhView& bv, int hint, double ox, double oy,
                                           double oz, double dx, double dy, double dz, double A,
-                                          double& bt, int& bi, CullStats& cs, Clock& clk) {
+                                          double& bt, int& bi, CullStats& cs, Clock& clk,
+                                          bool& trapped) {
   bt = __builtin_inf();
   bi = -1;
+  trapped = false;
   const bool finite = (A > 0.0) && (A < 1e200);
   const double am = __builtin_fmax(__builtin_fabs(ox),
                                    __builtin_fmax(__builtin_fabs(oy), __builtin_fabs(oz)));
@@ -274,20 +294,28 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     bi = sweep_linear(geo, n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), bt);
     return true;
   }
+  bool fix = false, full = false;
   if (hint >= 0) {
-    test_sphere(lgeo[hint], hint, ox, oy, oz, dx, dy, dz, A, bt, bi);
+    const double4 sh = lgeo[hint];
+    double ch;
+    test_sphere(sh, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, &ch);
+    fix = bv.fixpoint && ch == 0.0 && sh.w >= 0x1p-700 && sh.w <= 0x1p700 && am <= 0x1p40;
     ++cs.spheres;
   }
   clk.mark(kSecQHint);
   for (int b = 0; b < bv.n_big; ++b) {
     const int idx = bv.big_idx[b];
-    if (idx != hint) test_sphere(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
+    if (idx != hint) full |= test_sphere(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
   }
   cs.spheres += bv.n_big;
   clk.mark(kSecQBig);
-  const bool done = grid_point_query(lgeo, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs.spheres);
+  const bool done =
+      grid_point_query(lgeo, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs.spheres, full);
   clk.mark(kSecQGrid);
-  if (done) return true;
+  if (done) {
+    trapped = fix && !full && bi == hint;
+    return true;
+  }
   if (!(am <= bv.r_check)) {
     // Far origin (e.g. inside the r=1000 ground): test [0, bt] against the
     // padded root box in FP64 (error ~1e-13 relative, far inside the pad). A
@@ -404,8 +432,9 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
                                              double& best_t, CullStats& cs) {
   double bt;
   int bi;
+  bool trapped;
   SectionClock<false> noclk;
-  if (!hit_quick(geo, geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs, noclk))
+  if (!hit_quick(geo, geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs, noclk, trapped))
     hit_traverse<false, false>(bv, bv.nodes, bv.leaf_idx, geo, hint, ox, oy, oz, dx, dy, dz, A,
                                bt, bi, cs);
   best_t = bt;
@@ -568,9 +597,16 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       } else {
         ++rays;
         if constexpr (kBVH) {
-          resolved =
-              hit_quick(geo, lgeo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi, cs, clk);
+          bool trapped;
+          resolved = hit_quick(geo, lgeo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi,
+                               cs, clk, trapped);
           pending = !resolved;
+          if (trapped && k < a.max_depth) {
+            // the reference traces the max_depth - k rays that remain, all at
+            // t = +-0 on this sphere, then returns black (pbi >= 0 below)
+            rays += (unsigned)(a.max_depth - k);
+            finish = true;
+          }
         } else {
           pbi = sweep_linear(geo, a.n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), pbt);
           cs.spheres += a.n;

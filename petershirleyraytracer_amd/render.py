@@ -49,6 +49,7 @@ def _camera_array(c: RtCamera) -> np.ndarray:
 
 
 FLAG_NO_CULL = 1
+FLAG_NO_FIXPOINT = 2  # trace provably trapped paths to max_depth (same bits, slower)
 
 
 def params(width: int, height: int, spp: int, max_depth: int = 50, seed: int = 0,
@@ -151,8 +152,11 @@ def stats_dict(s: RtStats) -> dict:
 
 def render(spheres, camera, width: int, height: int, spp: int, max_depth: int = 50,
            seed: int = 0, row_offset: int = 0, row_stride: int = 1, want_rgb: bool = True,
-           cull: bool = True):
+           cull: bool = True, fixpoint: bool = True):
     """One-shot render of the owned rows on the default device (RT_DEVICE).
+
+    cull=False forces the linear sweep; fixpoint=False traces provably trapped
+    paths to max_depth. Neither changes a bit of the output.
 
     Returns (accum[rows, W, 3] float64, rgb8[rows, W, 3] uint8 or None, stats dict).
     """
@@ -160,7 +164,7 @@ def render(spheres, camera, width: int, height: int, spp: int, max_depth: int = 
     sp, n = _spheres(spheres)
     cam = _camera(camera)
     p = params(width, height, spp, max_depth, seed, row_offset, row_stride,
-               0 if cull else FLAG_NO_CULL)
+               (0 if cull else FLAG_NO_CULL) | (0 if fixpoint else FLAG_NO_FIXPOINT))
     rows = L.rt_rows_owned(height, row_offset, row_stride)
     if rows <= 0:
         raise _lib.RtError(f"shard owns no rows: height={height} offset={row_offset} "

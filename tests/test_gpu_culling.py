@@ -113,3 +113,44 @@ def test_renders_of_culled_scenes_vs_oracle(oracle_mod):
         want, _, rays = oracle_mod.render(sph, cam, 48, 27, 3, threads=8)
         assert np.array_equal(bits(got), bits(want))
         assert st["rays"] == rays
+
+
+def test_trapped_termination_is_bit_identical(oracle_mod, final_scene):
+    """ending paths stuck at an exact C == 0 fixed point changes no
+    bit and no ray count; it removes most executed work on the final scene."""
+    cam = P.camera_look_at(aspect=160 / 90)
+    a, ra, sa = P.render(final_scene, cam, 160, 90, 8, fixpoint=True)
+    b, rb, sb = P.render(final_scene, cam, 160, 90, 8, fixpoint=False)
+    assert np.array_equal(bits(a), bits(b)) and np.array_equal(ra, rb)
+    assert sa["rays"] == sb["rays"]
+    assert sa["tests_executed"] < sb["tests_executed"] / 2, (sa, sb)
+    want, _, rays = oracle_mod.render(final_scene, cam, 160, 90, 8, threads=8)
+    assert np.array_equal(bits(a), bits(want)) and sa["rays"] == rays
+
+
+def _contact_scene(rng):
+    """Spheres on exact, representable positions: touching pairs, spheres
+    resting on a big ground sphere, duplicates, nested and coincident ones —
+    the places where an origin can sit on two surfaces at once."""
+    s = [[0.0, -1000.0, 0.0, 1000.0]]
+    for i in range(-4, 5):
+        for k in range(-3, 1):
+            r = float(rng.choice([0.25, 0.5, 0.125]))
+            s.append([i * 1.0, r, k * 1.0 - 2.0, r])          # resting on y = 0
+    s += [[0.0, 1.0, -3.0, 0.5], [1.0, 1.0, -3.0, 0.5]]     # touching pair
+    s += [[-1.0, 1.0, -3.0, 0.5], [-1.0, 1.0, -3.0, 0.5]]   # duplicates
+    s += [[2.0, 1.0, -3.0, 0.5], [2.0, 1.0, -3.0, 0.25]]    # nested
+    s += [[0.5, 2.0, -3.0, 0.5], [0.5, 2.0, -3.0, -0.5]]    # negative radius twin
+    return np.array(s)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_trapped_termination_contact_scenes(oracle_mod, seed):
+    sph = _contact_scene(np.random.default_rng(seed))
+    cam = P.camera_look_at((0.0, 2.0, 4.0), (0.0, 0.5, -2.0), vfov=50.0, aspect=64 / 40)
+    a, ra, sa = P.render(sph, cam, 64, 40, 6, seed=seed, fixpoint=True)
+    b, rb, sb = P.render(sph, cam, 64, 40, 6, seed=seed, fixpoint=False)
+    assert np.array_equal(bits(a), bits(b)) and np.array_equal(ra, rb)
+    assert sa["rays"] == sb["rays"]
+    want, _, rays = oracle_mod.render(sph, cam, 64, 40, 6, seed=seed, threads=8)
+    assert np.array_equal(bits(a), bits(want)) and sa["rays"] == rays
