@@ -231,6 +231,46 @@ BvhHost build_bvh(const rt_sphere* s, int n) {
     g.start[c + 1] = g.start[c] + (int32_t)cells[c].size();
     g.items.insert(g.items.end(), cells[c].begin(), cells[c].end());
   }
+
+  // neighbour lists: two padded balls that meet have padded boxes that meet,
+  // so both spheres share a cell (membership is conservative); candidates come
+  // from the cells under j's box, the exact test is the centre distance
+  out.nb_word.assign(n, -1);
+  std::vector<int32_t> seen(n, -1), nb;
+  for (const Prim& p : prims) {
+    const int j = p.idx;
+    int c0[3], c1[3];
+    for (int k = 0; k < 3; ++k) {
+      const double a = std::floor((p.box.lo[k] - eps - (double)g.flo[k]) * inv);
+      const double b = std::floor((p.box.hi[k] + eps - (double)g.flo[k]) * inv);
+      c0[k] = (int)std::max(0.0, std::min((double)g.dims[k] - 1, a));
+      c1[k] = (int)std::max(0.0, std::min((double)g.dims[k] - 1, b));
+    }
+    nb.clear();
+    bool many = false;
+    for (int z = c0[2]; z <= c1[2] && !many; ++z)
+      for (int y = c0[1]; y <= c1[1] && !many; ++y)
+        for (int x = c0[0]; x <= c1[0] && !many; ++x) {
+          const std::vector<int32_t>& cl = cells[cidx(x, y, z)];
+          for (int32_t k : cl) {
+            if (k == j || seen[k] == j) continue;
+            seen[k] = j;
+            const double dx = s[k].cx - s[j].cx, dy = s[k].cy - s[j].cy, dz = s[k].cz - s[j].cz;
+            const double reach = (radii[j] + radii[k] + 2.0 * out.pad) * (1.0 + 0x1p-30);
+            if (std::sqrt(dx * dx + dy * dy + dz * dz) <= reach) {
+              nb.push_back(k);
+              if ((int)nb.size() > kNbMax) {
+                many = true;
+                break;
+              }
+            }
+          }
+        }
+    if (many) continue;
+    std::sort(nb.begin(), nb.end());
+    out.nb_word[j] = ((int32_t)out.nb_items.size() << 4) | (int32_t)nb.size();
+    out.nb_items.insert(out.nb_items.end(), nb.begin(), nb.end());
+  }
   out.enabled = true;
   return out;
 }

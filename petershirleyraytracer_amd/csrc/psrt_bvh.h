@@ -32,6 +32,7 @@ static_assert(sizeof(BvhNode) == 32, "node layout");
 constexpr int kBvhMinSpheres = 17;   // below this the linear sweep wins
 constexpr double kBigRatio = 16.0;   // radius > 16 x median -> tested every ray
 constexpr int kLeafMax = 2;
+constexpr int kNbMax = 15;           // neighbour lists longer than this use the grid
 
 // Point-location grid over the same padded boxes: cell -> spheres whose padded
 // box overlaps the cell. A ray whose segment [o, o + closest*d] lies inside one
@@ -53,6 +54,12 @@ struct BvhHost {
   std::vector<BvhNode> nodes;  // DFS order + one trailing padding node
   std::vector<int32_t> leaf_idx;  // original sphere index per leaf slot
   std::vector<int32_t> big_idx;   // original indices tested on every ray
+  // Neighbour lists: for BVH sphere j, every BVH sphere k
+  // with |c_j - c_k| <= |r_j| + |r_k| + 2 pad (k != j), i.e. every sphere whose
+  // padded ball can meet j's. nb_word[j] = first << 4 | count (count <=
+  // kNbMax); -1 for big spheres and spheres with more neighbours (grid path).
+  std::vector<int32_t> nb_word;   // [n], by original index
+  std::vector<int32_t> nb_items;  // original indices
   double pad = 0.0;               // absolute box padding
   double r_check = 0.0;           // rays with |o|_inf > r_check use the linear sweep
   int depth = 0;

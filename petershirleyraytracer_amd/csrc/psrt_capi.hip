@@ -77,6 +77,8 @@ struct rt_context {
   int* d_big = nullptr;
   int* d_cell_start = nullptr;
   int* d_cell_items = nullptr;
+  int* d_nb_word = nullptr;
+  int* d_nb_items = nullptr;
   psrt::GridHost pgrid;  // point-location grid (host copy of the geometry)
   double pad = 0.0;
   int n_nodes = 0, n_big = 0, n_leaf = 0;
@@ -91,6 +93,8 @@ struct rt_context {
   size_t samples_cap = 0;  // doubles
   double* d_accum_tmp = nullptr;
   size_t accum_tmp_cap = 0;  // doubles
+  uint4* d_plist = nullptr;  // camera-ray candidate lists, one uint4 per owned pixel
+  size_t plist_cap = 0;      // records
   unsigned long long* d_counters = nullptr;  // [0] queue head, [1] rays, [2] tests, [3] boxes
   std::vector<hipEvent_t> ev;  // pairs around each trace launch
   int ev_used = 0;
@@ -187,6 +191,7 @@ int rt_context_destroy(rt_context* c) {
   (void)hipFree(c->d_inv_r);
   (void)hipFree(c->d_samples);
   (void)hipFree(c->d_accum_tmp);
+  (void)hipFree(c->d_plist);
   (void)hipFree(c->d_counters);
   (void)hipFree(c->d_nodes);
   (void)hipFree(c->d_leaf_geo);
@@ -194,6 +199,8 @@ int rt_context_destroy(rt_context* c) {
   (void)hipFree(c->d_big);
   (void)hipFree(c->d_cell_start);
   (void)hipFree(c->d_cell_items);
+  (void)hipFree(c->d_nb_word);
+  (void)hipFree(c->d_nb_items);
   for (auto e : c->ev) (void)hipEventDestroy(e);
   if (c->ev_all0) (void)hipEventDestroy(c->ev_all0);
   if (c->ev_all1) (void)hipEventDestroy(c->ev_all1);
@@ -240,8 +247,11 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
   (void)hipFree(c->d_big);
   (void)hipFree(c->d_cell_start);
   (void)hipFree(c->d_cell_items);
+  (void)hipFree(c->d_nb_word);
+  (void)hipFree(c->d_nb_items);
   c->d_nodes = nullptr, c->d_leaf_geo = nullptr, c->d_leaf_idx = nullptr, c->d_big = nullptr;
   c->d_cell_start = nullptr, c->d_cell_items = nullptr;
+  c->d_nb_word = nullptr, c->d_nb_items = nullptr;
   c->bvh = b.enabled;
   c->n_nodes = c->n_big = c->n_leaf = 0;
   if (b.enabled) {
@@ -274,6 +284,13 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
     if (!b.grid.items.empty())
       HIP_TRY(hipMemcpy(c->d_cell_items, b.grid.items.data(), b.grid.items.size() * sizeof(int),
                         hipMemcpyHostToDevice));
+    const size_t nw = b.nb_word.size(), nn = std::max<size_t>(1, b.nb_items.size());
+    HIP_TRY(hipMalloc(&c->d_nb_word, std::max<size_t>(1, nw) * sizeof(int)));
+    HIP_TRY(hipMalloc(&c->d_nb_items, nn * sizeof(int)));
+    if (nw) HIP_TRY(hipMemcpy(c->d_nb_word, b.nb_word.data(), nw * sizeof(int), hipMemcpyHostToDevice));
+    if (!b.nb_items.empty())
+      HIP_TRY(hipMemcpy(c->d_nb_items, b.nb_items.data(), b.nb_items.size() * sizeof(int),
+                        hipMemcpyHostToDevice));
   }
   return RT_OK;
 }
@@ -290,6 +307,10 @@ static psrt::BvhView bvh_view(const rt_context* c) {
   v.r_check = c->r_check;
   v.cell_start = c->d_cell_start;
   v.cell_items = c->d_cell_items;
+  v.nb_word = c->d_nb_word;
+  v.nb_items = c->d_nb_items;
+  v.nb_c2 = 0.25 * c->pad * c->pad;
+  if (std::getenv("PSRT_NO_NEIGHBORS")) v.nb_c2 = -1.0;  // A/B knob: C^2 <= -r^2 never holds
   // grid bounds / scale in FP32, as used: the cell index of the device is a
   // function of these exact float values, and the host places each sphere in
   // every cell its padded box overlaps under the SAME float cell boundaries
@@ -383,7 +404,44 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   const bool use_bvh = c->bvh && !(p->flags & RT_FLAG_NO_CULL);
   psrt::BvhView bv = bvh_view(c);
   bv.fixpoint = !(p->flags & RT_FLAG_NO_FIXPOINT) && !std::getenv("PSRT_NO_FIXPOINT");
+  // camera-ray candidate lists: BVH scenes whose indices fit uint16 and whose
+  // camera lies inside the range the pad covers (|o|_inf <= r_check)
+  const double om = std::max(std::fabs(c->cam.origin[0]),
+                             std::max(std::fabs(c->cam.origin[1]), std::fabs(c->cam.origin[2])));
+  const bool camlist = use_bvh && c->n < (int)psrt::kCamOverflow && om <= c->r_check &&
+                       !std::getenv("PSRT_NO_CAMLIST");
+  if (camlist && c->plist_cap < P) {
+    (void)hipFree(c->d_plist);
+    c->d_plist = nullptr;
+    c->plist_cap = 0;
+    HIP_TRY(hipMalloc(&c->d_plist, P * sizeof(uint4)));
+    c->plist_cap = P;
+  }
   HIP_TRY(hipEventRecord(c->ev_all0, st));
+  if (camlist) {
+    psrt::CamListArgs la{};
+    for (int k = 0; k < 3; ++k) {
+      la.org[k] = c->cam.origin[k];
+      la.llc[k] = c->cam.lower_left[k];
+      la.hor[k] = c->cam.horizontal[k];
+      la.ver[k] = c->cam.vertical[k];
+    }
+    la.width = p->width;
+    la.height = p->height;
+    la.row_offset = p->row_offset;
+    la.row_stride = p->row_stride;
+    la.rows = rows;
+    la.leaf_geo = c->d_leaf_geo;
+    la.leaf_idx = c->d_leaf_idx;
+    la.n_leaf = c->n_leaf;
+    la.pad = c->pad;
+    la.plist = c->d_plist;
+    const dim3 lg((p->width + psrt::kCamTile - 1) / psrt::kCamTile,
+                  (rows + psrt::kCamTile - 1) / psrt::kCamTile);
+    hipLaunchKernelGGL(psrt::psrt_camera_lists, lg, dim3(64), 0, st, la);
+    HIP_TRY(hipGetLastError());
+    bv.plist = c->d_plist;
+  }
   for (int ch = 0; ch < nchunks; ++ch) {
     const int s0 = (int)(ch * s_chunk);
     const int sc = (int)std::min<size_t>(s_chunk, (size_t)(p->spp - s0));

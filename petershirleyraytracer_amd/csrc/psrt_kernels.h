@@ -41,6 +41,29 @@ struct BvhView {
   float glo[3], ghi[3], ginv, gmargin;  // FP32 copies (conservative use only)
   int gdims[3];
   int fixpoint;  // end provably trapped paths early (hit_quick; RT_FLAG_NO_FIXPOINT clears it)
+  // per-pixel candidate lists for camera rays (psrt_camera_lists), or nullptr:
+  // {count | idx0 << 16, idx1 | idx2 << 16, ...}: up to 7 BVH-sphere indices
+  // (uint16); count 0xFFFF = overflow (the ray walks the BVH)
+  const uint4* __restrict__ plist;
+  // neighbour lists (psrt_bvh.h): nb_word[j] = first << 4 | count, -1 = grid
+  const int* __restrict__ nb_word;
+  const int* __restrict__ nb_items;
+  double nb_c2;  // (pad/2)^2: C <= 0 or C^2 <= nb_c2 * r^2 puts o in j's padded ball
+};
+
+constexpr int kCamTile = 8;         // camera-list tiles are 8 x 8 pixels (one wave)
+constexpr int kCamTileCap = 1024;   // tile candidates held in LDS
+constexpr int kCamPixelCap = 7;     // candidates per pixel record
+constexpr unsigned kCamOverflow = 0xFFFFu;
+
+struct CamListArgs {
+  double org[3], llc[3], hor[3], ver[3];
+  int width, height, row_offset, row_stride, rows;
+  const double4* __restrict__ leaf_geo;  // BVH spheres {cx, cy, cz, r*r} per leaf slot
+  const int* __restrict__ leaf_idx;      // original index per leaf slot
+  int n_leaf;
+  double pad;                            // BVH box padding (absolute)
+  uint4* __restrict__ plist;             // [rows * width]
 };
 
 struct ReduceArgs {
@@ -57,6 +80,7 @@ template <bool kBVH, bool kStamps, bool kLds>
 __global__ void psrt_trace(const double4* __restrict__ geo, const double* __restrict__ inv_r,
                            double* __restrict__ samples, TraceArgs a, BvhView bv);
 __global__ void psrt_reduce(ReduceArgs a);
+__global__ void psrt_camera_lists(CamListArgs a);
 __global__ void psrt_quantize(const double* __restrict__ accum, unsigned char* __restrict__ rgb8,
                               unsigned n, int spp);
 __global__ void psrt_probe_hit(const double4* __restrict__ geo, const double* __restrict__ inv_r,

@@ -282,7 +282,8 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
                                           const BvhView& bv, int hint, double ox, double oy,
                                           double oz, double dx, double dy, double dz, double A,
                                           double& bt, int& bi, CullStats& cs, Clock& clk,
-                                          bool& trapped) {
+                                          bool& trapped, unsigned q,
+                                          const int* __restrict__ lnb) {
   bt = __builtin_inf();
   bi = -1;
   trapped = false;
@@ -295,12 +296,25 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     return true;
   }
   bool fix = false, full = false;
+  int nbw = -1;
+  // camera ray: the pixel's candidate list (psrt_camera_lists), loaded early
+  uint4 rec = make_uint4(kCamOverflow, 0u, 0u, 0u);
+  if (hint < 0 && bv.plist) rec = bv.plist[q];
   if (hint >= 0) {
     const double4 sh = lgeo[hint];
     double ch;
     test_sphere(sh, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, &ch);
     fix = bv.fixpoint && ch == 0.0 && sh.w >= 0x1p-700 && sh.w <= 0x1p700 && am <= 0x1p40;
     ++cs.spheres;
+    // Neighbour path: the hint sphere j was hit at bt and o
+    // lies within pad/2 of its surface, so the segment [o, o + bt d] (both
+    // ends in the ball of radius r_j + pad/2; the far end is a root of j, good
+    // to ~2^-19 S) stays in that ball. A sphere with an accepted root t <= bt
+    // has its hit point there and within the root error of its own surface,
+    // so its centre lies within r_j + r_k + pad of c_j: it is j's neighbour.
+    if (bi == hint && am <= bv.r_check && bv.nb_c2 >= 0.0 &&
+        (ch <= 0.0 || ch * ch <= bv.nb_c2 * sh.w))
+      nbw = lnb[hint];
   }
   clk.mark(kSecQHint);
   for (int b = 0; b < bv.n_big; ++b) {
@@ -309,6 +323,28 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
   }
   cs.spheres += bv.n_big;
   clk.mark(kSecQBig);
+  if (nbw >= 0) {
+    const int first = nbw >> 4, cnt = nbw & 15;
+    for (int e = 0; e < cnt; ++e) {
+      const int idx = bv.nb_items[first + e];
+      full |= test_sphere(lgeo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
+    }
+    cs.spheres += cnt;
+    trapped = fix && !full && bi == hint;
+    return true;
+  }
+  const unsigned ncand = rec.x & 0xFFFFu;
+  if (ncand != kCamOverflow) {  // every BVH sphere a ray of this pixel can hit is listed
+    uint64_t lo = rec.x | (uint64_t)rec.y << 32, hi = rec.z | (uint64_t)rec.w << 32;
+    for (unsigned e = 0; e < ncand; ++e) {
+      lo = (lo >> 16) | (hi << 48);
+      hi >>= 16;
+      const int idx = (int)(lo & 0xFFFFu);
+      test_sphere(lgeo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
+    }
+    cs.spheres += ncand;
+    return true;
+  }
   const bool done =
       grid_point_query(lgeo, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs.spheres, full);
   clk.mark(kSecQGrid);
@@ -434,7 +470,8 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
   int bi;
   bool trapped;
   SectionClock<false> noclk;
-  if (!hit_quick(geo, geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs, noclk, trapped))
+  if (!hit_quick(geo, geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs, noclk, trapped,
+                 0u, bv.nb_word))
     hit_traverse<false, false>(bv, bv.nodes, bv.leaf_idx, geo, hint, ox, oy, oz, dx, dy, dz, A,
                                bt, bi, cs);
   best_t = bt;
@@ -466,6 +503,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   __shared__ double4 s_geo[kLds ? kLdsSpheres : 1];
   __shared__ double s_inv[kLds ? kLdsSpheres : 1];
   __shared__ int s_leaf[kLds ? kLdsSpheres : 1];
+  __shared__ int s_nb[kLds ? kLdsSpheres : 1];
   // camera basis (only the refill block reads it): from LDS rather than held
   // in 24 SGPRs across the loop, which spills them into VGPR lanes
   __shared__ double s_cam[12];
@@ -478,12 +516,14 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     for (int e = threadIdx.x; e < 2 * (bv.n_nodes + 1); e += blockDim.x) s_nodes[e] = bv.nodes[e];
     for (int e = threadIdx.x; e < a.n; e += blockDim.x) s_geo[e] = geo[e], s_inv[e] = inv_r[e];
     for (int e = threadIdx.x; e < bv.n_leaf; e += blockDim.x) s_leaf[e] = bv.leaf_idx[e];
+    for (int e = threadIdx.x; e < a.n; e += blockDim.x) s_nb[e] = bv.nb_word[e];
   }
   __syncthreads();
   const float4* __restrict__ nodes = kLds ? s_nodes : bv.nodes;
   const double4* __restrict__ lgeo = kLds ? s_geo : geo;
   const double* __restrict__ linv = kLds ? s_inv : inv_r;
   const int* __restrict__ lleaf = (kLds && PSRT_LDS_LEAVES) ? s_leaf : bv.leaf_idx;
+  const int* __restrict__ lnb = kLds ? s_nb : bv.nb_word;
 
   // wave-uniform work window
   uint64_t win_base = 0;
@@ -599,7 +639,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
         if constexpr (kBVH) {
           bool trapped;
           resolved = hit_quick(geo, lgeo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi,
-                               cs, clk, trapped);
+                               cs, clk, trapped, q, lnb);
           pending = !resolved;
           if (trapped && k < a.max_depth) {
             // the reference traces the max_depth - k rays that remain, all at
@@ -758,6 +798,114 @@ __global__ __launch_bounds__(256) void psrt_reduce(ReduceArgs a) {
       a.rgb8[(size_t)q * 3 + ch] = (unsigned char)(int)(255.999 * x);
     }
   }
+}
+
+// ---- camera-ray candidate lists ------------------------------
+//
+// Every camera ray of pixel (i, j) has direction d = ((llc + u*h) + v*vv) - o
+// (camera.h:25-28) with u in [i/(W-1), (i+1)/(W-1)], v in [j/(H-1), (j+1)/(H-1)]
+// (main.cc:80-81): a parallelogram of directions, inside the cone around the
+// pixel centre's direction whose half-angle reaches the four corners (the
+// angle to the axis is quasi-convex, so its maximum is at a corner). A BVH
+// sphere can return an accepted root only if its padded ball (r + pad, the
+// same pad that bounds the root error for the BVH boxes) meets that cone. The
+// cone test below is done in FP64 with the angle widened by 1e-9 rad and the
+// radius by 2^-20, margins far above its own rounding (~1e-15). Camera rays
+// then test the big spheres and the pixel's list only.
+
+__device__ __forceinline__ void cam_dir(const CamListArgs& a, double u, double v, double d[3]) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) d[k] = ((a.llc[k] + u * a.hor[k]) + v * a.ver[k]) - a.org[k];
+}
+
+struct Cone {
+  double ax, ay, az, ca, sa;  // unit axis, cos / sin of the (widened) half-angle
+  bool ok;
+};
+
+__device__ __forceinline__ Cone cam_cone(const CamListArgs& a, double u0, double u1, double v0,
+                                         double v1) {
+  Cone c;
+  double d[3];
+  cam_dir(a, 0.5 * (u0 + u1), 0.5 * (v0 + v1), d);
+  const double il = 1.0 / __builtin_sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
+  c.ax = d[0] * il, c.ay = d[1] * il, c.az = d[2] * il;
+  double cmin = 1.0;
+  const double us[2] = {u0, u1}, vs[2] = {v0, v1};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    cam_dir(a, us[e & 1], vs[e >> 1], d);
+    const double l = __builtin_sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
+    cmin = __builtin_fmin(cmin, ((c.ax * d[0] + c.ay * d[1]) + c.az * d[2]) / l);
+  }
+  c.ca = cmin - 1e-9;  // cos(alpha + delta) >= cos(alpha) - delta: widens by >= 1e-9 rad
+  c.sa = __builtin_sqrt(__builtin_fmax(0.0, 1.0 - c.ca * c.ca));
+  c.ok = c.ca > 0.1 && il > 0.0 && il < 1e300;  // narrow, finite cone (else: no lists)
+  return c;
+}
+
+// Does the ball (centre s.xyz, radius sqrt(s.w) + pad) meet the cone with apex o?
+__device__ __forceinline__ bool cone_meets(const Cone& c, const CamListArgs& a, const double4 s) {
+  const double cx = s.x - a.org[0], cy = s.y - a.org[1], cz = s.z - a.org[2];
+  const double l2 = (cx * cx + cy * cy) + cz * cz;
+  const double R = (__builtin_sqrt(s.w) + a.pad) * (1.0 + 0x1p-20);
+  if (!(l2 > R * R * (1.0 + 0x1p-20))) return true;  // apex inside / near the ball (or NaN)
+  const double l = __builtin_sqrt(l2);
+  const double cb = ((c.ax * cx + c.ay * cy) + c.az * cz) / l;
+  if (cb >= c.ca) return true;  // centre inside the cone
+  const double sb = __builtin_sqrt(__builtin_fmax(0.0, 1.0 - cb * cb));
+  // angle(axis, centre) - alpha must be <= asin(R / l) (<= pi/2)
+  const double cosd = cb * c.ca + sb * c.sa, sind = sb * c.ca - cb * c.sa;
+  return cosd >= 0.0 && sind <= R / l;
+}
+
+__global__ __launch_bounds__(64) void psrt_camera_lists(CamListArgs a) {
+  __shared__ int s_tile[kCamTileCap];
+  const unsigned lane = __lane_id();
+  const int x0 = blockIdx.x * kCamTile, r0 = blockIdx.y * kCamTile;
+  const int x1 = min(x0 + kCamTile, a.width), r1 = min(r0 + kCamTile, a.rows);
+  const int px = x0 + (int)(lane % kCamTile), rk = r0 + (int)(lane / kCamTile);
+  const double iw = 1.0 / (double)(a.width - 1), ih = 1.0 / (double)(a.height - 1);
+  // reference rows j = H-1-r fall as the shard row rk rises (main.cc:72)
+  const int jhi = a.height - 1 - (a.row_offset + r0 * a.row_stride);
+  const int jlo = a.height - 1 - (a.row_offset + (r1 - 1) * a.row_stride);
+  // u, v bounds: i/(W-1) etc. widened by a relative 2^-40 (covers the rounding
+  // of i + random_double() and of the division, main.cc:80-81)
+  const double wid = 1.0 + 0x1p-40;
+  const Cone tc = cam_cone(a, x0 * iw / wid, x1 * iw * wid, jlo * ih / wid, (jhi + 1) * ih * wid);
+  int cnt = 0;
+  bool over = !tc.ok;
+  for (int base = 0; base < a.n_leaf && !over; base += 64) {
+    const int k = base + (int)lane;
+    const bool cand = k < a.n_leaf && cone_meets(tc, a, a.leaf_geo[k]);
+    const uint64_t m = __ballot(cand);
+    const int pos = cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+    if (cand && pos < kCamTileCap) s_tile[pos] = k;
+    cnt += __popcll(m);
+    if (cnt > kCamTileCap) over = true;
+  }
+  __syncthreads();
+  if (px >= a.width || rk >= a.rows) return;
+  const int j = a.height - 1 - (a.row_offset + rk * a.row_stride);
+  unsigned w[4] = {kCamOverflow, 0u, 0u, 0u};
+  if (!over) {
+    const Cone pc = cam_cone(a, px * iw / wid, (px + 1) * iw * wid, j * ih / wid, (j + 1) * ih * wid);
+    unsigned n = 0;
+    bool full = !pc.ok;
+    for (int e = 0; e < cnt && !full; ++e) {
+      const int k = s_tile[e];
+      if (!cone_meets(pc, a, a.leaf_geo[k])) continue;
+      if (n == (unsigned)kCamPixelCap) {
+        full = true;
+        break;
+      }
+      ++n;  // slot n of 8 uint16 (slot 0 = count)
+      w[n >> 1] |= (unsigned)a.leaf_idx[k] << ((n & 1) * 16);
+    }
+    if (!full) w[0] = (w[0] & 0xFFFF0000u) | n;
+  }
+  a.plist[(size_t)rk * a.width + px] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 __global__ __launch_bounds__(256) void psrt_quantize(const double* __restrict__ accum,

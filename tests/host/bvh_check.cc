@@ -85,6 +85,31 @@ static void check_scene(const std::vector<rt_sphere>& s) {
           CHECK(found, "sphere listed in every touched cell");
         }
   }
+  // neighbour lists: exactly the BVH spheres within |r_j| + |r_k| + 2 pad, or -1
+  std::vector<char> big(n, 0);
+  for (int i : b.big_idx) big[i] = 1;
+  CHECK((int)b.nb_word.size() == n, "one neighbour word per sphere");
+  for (int j = 0; j < n; ++j) {
+    if (big[j]) {
+      CHECK(b.nb_word[j] == -1, "big spheres use the grid path");
+      continue;
+    }
+    std::vector<int> want;
+    for (int k = 0; k < n; ++k) {
+      if (k == j || big[k]) continue;
+      const double dx = s[k].cx - s[j].cx, dy = s[k].cy - s[j].cy, dz = s[k].cz - s[j].cz;
+      const double reach = (std::fabs(s[j].r) + std::fabs(s[k].r) + 2.0 * b.pad) * (1.0 + 0x1p-30);
+      if (std::sqrt(dx * dx + dy * dy + dz * dz) <= reach) want.push_back(k);
+    }
+    const int w = b.nb_word[j];
+    if ((int)want.size() > psrt::kNbMax) {
+      CHECK(w == -1, "long neighbour lists fall back to the grid");
+      continue;
+    }
+    CHECK(w >= 0 && (w & 15) == (int)want.size(), "neighbour count");
+    for (int e = 0; e < (int)want.size(); ++e)
+      CHECK(b.nb_items[(w >> 4) + e] == want[e], "neighbour list = all spheres in reach, sorted");
+  }
   std::printf("ok %d %zu %zu %zu\n", m, b.big_idx.size(), g.start.size() - 1, g.items.size());
 }
 

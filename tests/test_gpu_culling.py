@@ -154,3 +154,42 @@ def test_trapped_termination_contact_scenes(oracle_mod, seed):
     assert sa["rays"] == sb["rays"]
     want, _, rays = oracle_mod.render(sph, cam, 64, 40, 6, seed=seed, threads=8)
     assert np.array_equal(bits(a), bits(want)) and sa["rays"] == rays
+
+
+def test_camera_lists_are_bit_identical(oracle_mod, final_scene, monkeypatch):
+    """camera rays tested against per-pixel candidate lists give
+    the same frame as the BVH walk, for the benchmark camera and for cameras
+    close to / inside spheres, wide and narrow fields, and a 1:3 shard."""
+    cams = [P.camera_look_at(aspect=96 / 64),
+            P.camera_look_at((4.0, 1.0, 0.5), (4.0, 1.0, -3.0), vfov=90.0, aspect=96 / 64),
+            P.camera_look_at((-4.0, 1.2, 0.0), (0.0, 0.2, 0.0), vfov=120.0, aspect=96 / 64),
+            P.camera_look_at((0.0, 0.3, 2.0), (0.0, 0.2, -5.0), vfov=5.0, aspect=96 / 64)]
+    for cam in cams:
+        for off, stride in ((0, 1), (1, 3)):
+            a, _, sa = P.render(final_scene, cam, 96, 64, 3, row_offset=off, row_stride=stride)
+            monkeypatch.setenv("PSRT_NO_CAMLIST", "1")
+            b, _, sb = P.render(final_scene, cam, 96, 64, 3, row_offset=off, row_stride=stride)
+            monkeypatch.delenv("PSRT_NO_CAMLIST")
+            assert np.array_equal(bits(a), bits(b)) and sa["rays"] == sb["rays"]
+            want, _, rays = oracle_mod.render(final_scene, cam, 96, 64, 3, row_offset=off,
+                                              row_stride=stride, threads=8)
+            assert np.array_equal(bits(a), bits(want)) and sa["rays"] == rays
+
+
+def test_neighbour_lists_are_bit_identical(oracle_mod, final_scene, monkeypatch):
+    """rays that re-hit their start sphere test only its
+    neighbours; the frames equal the grid/BVH path's and the oracle's, on the
+    final scene and on contact scenes (touching, duplicate, nested spheres)."""
+    scenes = [(final_scene, P.camera_look_at(aspect=96 / 64))]
+    for seed in (1, 2):
+        scenes.append((_contact_scene(np.random.default_rng(seed)),
+                       P.camera_look_at((0.0, 2.0, 4.0), (0.0, 0.5, -2.0), vfov=50.0,
+                                        aspect=96 / 64)))
+    for sph, cam in scenes:
+        a, _, sa = P.render(sph, cam, 96, 64, 4)
+        monkeypatch.setenv("PSRT_NO_NEIGHBORS", "1")
+        b, _, sb = P.render(sph, cam, 96, 64, 4)
+        monkeypatch.delenv("PSRT_NO_NEIGHBORS")
+        assert np.array_equal(bits(a), bits(b)) and sa["rays"] == sb["rays"]
+        want, _, rays = oracle_mod.render(sph, cam, 96, 64, 4, threads=8)
+        assert np.array_equal(bits(a), bits(want)) and sa["rays"] == rays
