@@ -55,6 +55,19 @@ uint64_t splitmix64_host(uint64_t x) {
   return z ^ (z >> 31);
 }
 
+// Magic numbers for n / d, n < 2^32 (psrt_kernels.h FastDiv): l = ceil(log2 d),
+// m = floor(2^32 (2^l - d) / d) + 1.
+psrt::FastDiv fast_div_make(unsigned d) {
+  unsigned l = 0;
+  while (l < 32 && (1ull << l) < d) ++l;
+  psrt::FastDiv f;
+  f.m = (unsigned)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+  f.sh1 = l ? 1u : 0u;
+  f.sh2 = l ? l - 1 : 0u;
+  f.d = d;
+  return f;
+}
+
 size_t sample_buffer_cap_bytes() {
   const char* e = std::getenv("PSRT_SAMPLE_BUF_MB");
   size_t mb = e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)4096;
@@ -176,7 +189,7 @@ int rt_context_create(int device, rt_context** out) {
                                                         psrt::kTraceBlock, 0));
   c->grid_bvh = c->cus * (per_cu < 1 ? 1 : per_cu);
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  HIP_TRY(hipMalloc(&c->d_counters, 32 * sizeof(unsigned long long)));
+  HIP_TRY(hipMalloc(&c->d_counters, 64 * sizeof(unsigned long long)));
   HIP_TRY(hipEventCreate(&c->ev_all0));
   HIP_TRY(hipEventCreate(&c->ev_all1));
   *out = c;
@@ -384,10 +397,11 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   ta.row_stride = p->row_stride;
   ta.pixels = (unsigned)P;
   ta.seedmix = splitmix64_host(p->seed);
+  ta.div_w = fast_div_make((unsigned)p->width);
   ta.work_counter = c->d_counters;
   ta.ray_counter = c->d_counters + 1;
 
-  HIP_TRY(hipMemsetAsync(c->d_counters + 1, 0, 31 * sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(c->d_counters + 1, 0, 63 * sizeof(unsigned long long), st));
   const bool stamps = std::getenv("PSRT_STAMPS") != nullptr;  // diagnostic build
   ta.stamps = c->d_counters + 8;
   {
@@ -447,6 +461,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     const int sc = (int)std::min<size_t>(s_chunk, (size_t)(p->spp - s0));
     ta.s_begin = s0;
     ta.s_count = sc;
+    ta.div_s = fast_div_make((unsigned)sc);
     ta.total_units = (uint64_t)P * sc;
     HIP_TRY(hipMemsetAsync(c->d_counters, 0, sizeof(unsigned long long), st));
     HIP_TRY(hipEventRecord(c->ev[2 * ch], st));
@@ -512,8 +527,19 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   c->last.kernel_ms = kms;
   c->last.total_ms = all;
   if (std::getenv("PSRT_STAMPS")) {
-    unsigned long long sec[12];
+    unsigned long long sec[32];
     HIP_TRY(hipMemcpy(sec, c->d_counters + 8, sizeof sec, hipMemcpyDeviceToHost));
+    static const char* names[10] = {"refill", "store", "hit", "hint", "nb", "cam",
+                                    "grid", "walk", "trial", "scatter"};
+    std::string u = "{\"psrt_util\": {";
+    for (int k = 0; k < 10; ++k) {
+      char b[128];
+      const double w = (double)sec[12 + 2 * k], l = (double)sec[13 + 2 * k];
+      std::snprintf(b, sizeof b, "%s\"%s\": [%.4g, %.2f]", k ? ", " : "", names[k], w,
+                    w > 0 ? l / w : 0.0);
+      u += b;
+    }
+    std::fprintf(stderr, "%s}}\n", u.c_str());
     double tot = 0;
     for (int k = 0; k < 8; ++k) tot += (double)sec[k];
     std::fprintf(stderr,

@@ -11,6 +11,12 @@ constexpr unsigned kWorkChunk = 1024;  // units a wave takes per queue dequeue
 constexpr int kLdsNodes = 640;         // BVH nodes staged per workgroup (20 KB of LDS)
 constexpr int kLdsSpheres = 640;       // spheres staged per workgroup (25 KB of LDS)
 
+// Division of n < 2^32 by an invariant d: q = (t + ((n - t) >> sh1)) >> sh2,
+// t = mulhi(m, n) (host: FastDiv::make).
+struct FastDiv {
+  unsigned m, sh1, sh2, d;
+};
+
 struct TraceArgs {
   int n;               // spheres (geo: {cx, cy, cz, r*r}, inv_r: 1.0/r)
   double org[3], llc[3], hor[3], ver[3];
@@ -26,6 +32,7 @@ struct TraceArgs {
   unsigned batch;                   // parked lanes that trigger a batched BVH pass
   int rng_fill;                     // look-ahead trials per lane per iteration (min)
   unsigned refill_min;              // idle lanes that trigger the finish + refill block
+  FastDiv div_s, div_w;             // unit / s_count, q / width
 };
 
 struct BvhView {

@@ -36,9 +36,26 @@ enum Section {
   kSecQHint, kSecQBig, kSecQGrid, kSecCount  // hit_quick sub-sections (share of kSecHit)
 };
 
+// Lane utilisation probes (diagnostic build): per probe, wave executions and
+// active lanes, counted by the first active lane.
+enum Util { kURefill = 0, kUStore, kUHit, kUHint, kUNb, kUCam, kUGrid, kUWalk, kUTrial,
+            kUScatter, kUCount };
+
+__device__ __forceinline__ bool first_active_lane();
+
 template <bool kOn>
 struct SectionClock {
   uint64_t t = 0, acc[kSecCount] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned uw[kOn ? kUCount : 1] = {}, ul[kOn ? kUCount : 1] = {};
+  __device__ __forceinline__ void util(int u) {
+    if constexpr (kOn) {
+      const uint64_t m = __ballot(1);
+      if (first_active_lane()) {
+        uw[u] += 1;
+        ul[u] += (unsigned)__popcll(m);
+      }
+    }
+  }
   __device__ __forceinline__ void start() {
     if constexpr (kOn) t = now();
   }
@@ -57,6 +74,19 @@ struct SectionClock {
     return v;
   }
 };
+
+struct RefillConst {
+  double cam[12];  // origin, lower_left, horizontal, vertical
+  double wm1, hm1;  // (double)(W - 1), (double)(H - 1)   main.cc:80-81
+  uint64_t seedmix;
+  FastDiv div_s, div_w;
+  int hm1_i, row_offset, row_stride, s_begin;
+};
+
+__device__ __forceinline__ unsigned fast_div(unsigned n, const FastDiv& f) {
+  const unsigned t = __umulhi(f.m, n);
+  return (t + ((n - t) >> f.sh1)) >> f.sh2;
+}
 
 __device__ __forceinline__ unsigned mbcnt64(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
@@ -301,6 +331,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
   uint4 rec = make_uint4(kCamOverflow, 0u, 0u, 0u);
   if (hint < 0 && bv.plist) rec = bv.plist[q];
   if (hint >= 0) {
+    clk.util(kUHint);
     const double4 sh = lgeo[hint];
     double ch;
     test_sphere(sh, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, &ch);
@@ -324,6 +355,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
   cs.spheres += bv.n_big;
   clk.mark(kSecQBig);
   if (nbw >= 0) {
+    clk.util(kUNb);
     const int first = nbw >> 4, cnt = nbw & 15;
     for (int e = 0; e < cnt; ++e) {
       const int idx = bv.nb_items[first + e];
@@ -335,6 +367,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
   }
   const unsigned ncand = rec.x & 0xFFFFu;
   if (ncand != kCamOverflow) {  // every BVH sphere a ray of this pixel can hit is listed
+    clk.util(kUCam);
     uint64_t lo = rec.x | (uint64_t)rec.y << 32, hi = rec.z | (uint64_t)rec.w << 32;
     for (unsigned e = 0; e < ncand; ++e) {
       lo = (lo >> 16) | (hi << 48);
@@ -345,6 +378,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     cs.spheres += ncand;
     return true;
   }
+  clk.util(kUGrid);
   const bool done =
       grid_point_query(lgeo, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs.spheres, full);
   clk.mark(kSecQGrid);
@@ -504,14 +538,27 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   __shared__ double s_inv[kLds ? kLdsSpheres : 1];
   __shared__ int s_leaf[kLds ? kLdsSpheres : 1];
   __shared__ int s_nb[kLds ? kLdsSpheres : 1];
-  // camera basis (only the refill block reads it): from LDS rather than held
-  // in 24 SGPRs across the loop, which spills them into VGPR lanes
-  __shared__ double s_cam[12];
+  // Constants only the refill block reads (camera basis, image size, the
+  // divisions' magic numbers, the seed) live in LDS and are re-read on every
+  // refill through an offset the compiler cannot see through: held across
+  // the loop they would take ~40 registers and spill to scratch.
+  __shared__ RefillConst s_rc;
   if (threadIdx.x < 12)
-    s_cam[threadIdx.x] = threadIdx.x < 3   ? a.org[threadIdx.x]
-                         : threadIdx.x < 6 ? a.llc[threadIdx.x - 3]
-                         : threadIdx.x < 9 ? a.hor[threadIdx.x - 6]
-                                           : a.ver[threadIdx.x - 9];
+    s_rc.cam[threadIdx.x] = threadIdx.x < 3   ? a.org[threadIdx.x]
+                            : threadIdx.x < 6 ? a.llc[threadIdx.x - 3]
+                            : threadIdx.x < 9 ? a.hor[threadIdx.x - 6]
+                                              : a.ver[threadIdx.x - 9];
+  if (threadIdx.x == 0) {
+    s_rc.wm1 = (double)(a.width - 1);
+    s_rc.hm1 = (double)(a.height - 1);
+    s_rc.seedmix = a.seedmix;
+    s_rc.div_s = a.div_s;
+    s_rc.div_w = a.div_w;
+    s_rc.hm1_i = a.height - 1;
+    s_rc.row_offset = a.row_offset;
+    s_rc.row_stride = a.row_stride;
+    s_rc.s_begin = a.s_begin;
+  }
   if constexpr (kLds) {  // host guarantees n_nodes < kLdsNodes and n <= kLdsSpheres
     for (int e = threadIdx.x; e < 2 * (bv.n_nodes + 1); e += blockDim.x) s_nodes[e] = bv.nodes[e];
     for (int e = threadIdx.x; e < a.n; e += blockDim.x) s_geo[e] = geo[e], s_inv[e] = inv_r[e];
@@ -562,6 +609,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     if (run_block) {
       // sky (main.cc:46-48) x 0.5^k, or black; store
       if (done) {
+        clk.util(kUStore);
         double col_r = 0.0, col_g = 0.0, col_b = 0.0;
         if (pbi < 0 && a.max_depth >= 0) {
           const double y = (1.0 / __builtin_sqrt(A)) * dy;
@@ -587,21 +635,26 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
         nb = __shfl(nb, 0);
       }
       if (need) {
+        clk.util(kURefill);
         const uint64_t unit = rank < win_left ? win_base + rank : nb + (rank - win_left);
         if (unit < total) {  // total < 2^32 (host chunking)
-          q = (unsigned)unit / (unsigned)a.s_count;
-          sl = (unsigned)unit - q * (unsigned)a.s_count;
-          const unsigned row_k = q / (unsigned)a.width;
-          const unsigned i = q - row_k * (unsigned)a.width;
-          const int r = a.row_offset + (int)row_k * a.row_stride;
-          const int j = a.height - 1 - r;
-          const unsigned pix = (unsigned)j * (unsigned)a.width + i;
-          const unsigned s = (unsigned)a.s_begin + sl;
-          rng = splitmix64((((uint64_t)pix) << 32 | (uint64_t)s) ^ a.seedmix);
+          unsigned zo = 0;
+          asm volatile("" : "+v"(zo));  // keeps the LDS reads below inside the loop
+          const RefillConst& rc = *(const RefillConst*)((const char*)&s_rc + zo);
+          const FastDiv ds = rc.div_s, dw = rc.div_w;
+          q = fast_div((unsigned)unit, ds);
+          sl = (unsigned)unit - q * ds.d;
+          const unsigned row_k = fast_div(q, dw);
+          const unsigned i = q - row_k * dw.d;
+          const int r = rc.row_offset + (int)row_k * rc.row_stride;
+          const int j = rc.hm1_i - r;
+          const unsigned pix = (unsigned)j * dw.d + i;
+          const unsigned s = (unsigned)rc.s_begin + sl;
+          rng = splitmix64((((uint64_t)pix) << 32 | (uint64_t)s) ^ rc.seedmix);
           // main.cc:80-81, camera.h:25-28
-          const double u = ((double)i + random_double(rng)) / (double)(a.width - 1);
-          const double v = ((double)j + random_double(rng)) / (double)(a.height - 1);
-          const double* cam = s_cam;  // origin, lower_left, horizontal, vertical
+          const double u = ((double)i + random_double(rng)) / rc.wm1;
+          const double v = ((double)j + random_double(rng)) / rc.hm1;
+          const double* cam = rc.cam;  // origin, lower_left, horizontal, vertical
           ox = cam[0], oy = cam[1], oz = cam[2];
           dx = ((cam[3] + u * cam[6]) + v * cam[9]) - ox;
           dy = ((cam[4] + u * cam[7]) + v * cam[10]) - oy;
@@ -636,6 +689,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
         finish = true;
       } else {
         ++rays;
+        clk.util(kUHit);
         if constexpr (kBVH) {
           bool trapped;
           resolved = hit_quick(geo, lgeo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi,
@@ -660,6 +714,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       const uint64_t movable = __ballot(active && !pending);
       if (pend != 0 && ((unsigned)__popcll(pend) >= a.batch || movable == 0)) {
         if (pending) {
+          clk.util(kUWalk);
           hit_traverse<kStamps, kLds && PSRT_LDS_LEAVES>(bv, nodes, lleaf, lgeo, hint, ox, oy,
                                                          oz, dx, dy, dz, A, pbt, pbi, cs);
           pending = false;
@@ -688,6 +743,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       for (int f = 0;; ++f) {
         if (f >= a.rng_fill && __ballot(want && qn == 0) == 0) break;
         const bool go = can_fill && qn < 2;
+        if (go) clk.util(kUTrial);
         uint32_t z, y, x;
         uint64_t nxt;
         rand31_x3(rng, z, y, x, nxt);  // z, y, x: g++'s draw order (vec3.h:78-81)
@@ -705,6 +761,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
 
     // ---- scatter: target = (p + n) + random_in_hemisphere(n)  (main.cc:42-43) ----
     if (resolved && !finish) {
+      clk.util(kUScatter);
       const HitRec h = hit_record_of(lgeo[hit], linv[hit], t, ox, oy, oz, dx, dy, dz);
       // vec3.h:78-81 random(-1, 1) from the queued draws; vec3.h:102-109 flip
       double rx = pm1_of(q0x), ry = pm1_of(q0y), rz = pm1_of(q0z);
@@ -736,6 +793,10 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     atomicAdd(a.stamps + 9, (unsigned long long)cs.wave_leaf_trips);
     atomicAdd(a.stamps + 10, (unsigned long long)cs.trav_rays);
     atomicAdd(a.stamps + 11, (unsigned long long)cs.leaf_visits);
+    for (int u = 0; u < kUCount; ++u) {
+      atomicAdd(a.stamps + 12 + 2 * u, (unsigned long long)clk.uw[u]);
+      atomicAdd(a.stamps + 13 + 2 * u, (unsigned long long)clk.ul[u]);
+    }
   }
 
   // rays / sphere tests / box tests of this wave -> one atomic each

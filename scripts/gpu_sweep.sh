@@ -13,4 +13,4 @@ for kv in ${SWEEP:-DEFAULT=1}; do
   python3 -c "import json; d=json.loads(open('gpurun_out/sweep_$i.log').read().strip().splitlines()[-1]); print('$kv', d['value'], d['roofline']['avg_launch_ms'])"
 done
 env ${STAMP_ENV:-DEFAULT=1} PSRT_STAMPS=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 1 ${BENCH_ARGS} > gpurun_out/bench_stamps.log 2>&1
-grep psrt_sections gpurun_out/bench_stamps.log | tail -1
+grep -E "psrt_sections|psrt_util" gpurun_out/bench_stamps.log | tail -2
