@@ -405,14 +405,14 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   const bool stamps = std::getenv("PSRT_STAMPS") != nullptr;  // diagnostic build
   ta.stamps = c->d_counters + 8;
   {
-    const char* e = std::getenv("PSRT_BATCH");  // tuning knob (default 18 of 64 lanes)
-    ta.batch = e ? (unsigned)std::atoi(e) : 18u;
+    const char* e = std::getenv("PSRT_BATCH");  // tuning knob (default 24 of 64 lanes)
+    ta.batch = e ? (unsigned)std::atoi(e) : 24u;
     if (ta.batch < 1) ta.batch = 1;
     const char* f = std::getenv("PSRT_RNG_FILL");  // tuning knob (default 2)
     ta.rng_fill = f ? std::atoi(f) : 2;
     if (ta.rng_fill < 0) ta.rng_fill = 0;
-    const char* r = std::getenv("PSRT_REFILL_MIN");  // tuning knob (default 8 of 64 lanes)
-    ta.refill_min = r ? (unsigned)std::atoi(r) : 8u;
+    const char* r = std::getenv("PSRT_REFILL_MIN");  // tuning knob (default 16 of 64 lanes)
+    ta.refill_min = r ? (unsigned)std::atoi(r) : 16u;
     if (ta.refill_min < 1) ta.refill_min = 1;
   }
   const bool use_bvh = c->bvh && !(p->flags & RT_FLAG_NO_CULL);

@@ -212,15 +212,15 @@ __device__ __forceinline__ bool test_sphere(const double4 s, int idx, double ox,
 }
 
 // Point query for a short segment [o, o + bt*d] (the common case: the ray
-// re-hit the sphere it starts on at t ~ 0). Returns 1 if resolved (cell
-// spheres tested, or the segment is outside the grid: no culled sphere can
-// be hit), 0 if the BVH must be walked.
-__device__ __forceinline__ int grid_point_query(const double4* __restrict__ lgeo,
-                                                const BvhView& bv, int hint, double ox,
-                                                double oy, double oz, double dx, double dy,
-                                                double dz, double A, double& bt, int& bi,
-                                                unsigned& tests, bool& full) {
-  if (!(bt < 1e30)) return 0;
+// re-hit the sphere it starts on at t ~ 0). Returns the cell whose spheres
+// are the only BVH spheres the segment can hit, kGridOutside when the segment
+// lies outside the grid (no BVH sphere can be hit), or kGridNone when it
+// cannot be bounded this way (the BVH must be walked).
+constexpr int kGridNone = -1, kGridOutside = -2;
+
+__device__ __forceinline__ int grid_locate(const BvhView& bv, double ox, double oy, double oz,
+                                           double dx, double dy, double dz, double bt) {
+  if (!(bt < 1e30)) return kGridNone;
   // FP32 is enough: the test is conservative and its error (~2^-22 of the
   // scene scale) is far inside the margin (pad/4, psrt_bvh.cpp)
   const float m = bv.gmargin;
@@ -239,17 +239,9 @@ __device__ __forceinline__ int grid_point_query(const double4* __restrict__ lgeo
     const int c1 = (int)__builtin_floorf((hi - glo) * bv.ginv);
     ci[k] = (c0 == c1 && c0 >= 0 && c0 < bv.gdims[k]) ? c0 : -1;
   }
-  if (outside) return 1;
-  if (ci[0] < 0 || ci[1] < 0 || ci[2] < 0) return 0;
-  const int cell = (ci[2] * bv.gdims[1] + ci[1]) * bv.gdims[0] + ci[0];
-  const int e0 = bv.cell_start[cell], e1 = bv.cell_start[cell + 1];
-  for (int e = e0; e < e1; ++e) {
-    const int idx = bv.cell_items[e];
-    if (idx == hint) continue;
-    full |= test_sphere(lgeo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
-    ++tests;
-  }
-  return 1;
+  if (outside) return kGridOutside;
+  if (ci[0] < 0 || ci[1] < 0 || ci[2] < 0) return kGridNone;
+  return (ci[2] * bv.gdims[1] + ci[1]) * bv.gdims[0] + ci[0];
 }
 
 __device__ __forceinline__ float tmax_up(double t) {
@@ -354,35 +346,49 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
   }
   cs.spheres += bv.n_big;
   clk.mark(kSecQBig);
+  // The candidate list of this ray, one of:
+  //   neighbour list of the hint sphere (nb path), the pixel's camera list,
+  //   or the grid cell holding [o, o + bt d];
+  // all three are walked by ONE loop below, so a wave whose lanes took
+  // different paths runs max(count) sphere tests instead of their sum.
+  const int* __restrict__ items = bv.nb_items;
+  int cnt = 0;
+  bool listed = true;
+  const unsigned ncand = rec.x & 0xFFFFu;
+  const bool cam = nbw < 0 && ncand != kCamOverflow;
+  uint64_t lo = rec.x | (uint64_t)rec.y << 32, hi = rec.z | (uint64_t)rec.w << 32;
   if (nbw >= 0) {
     clk.util(kUNb);
-    const int first = nbw >> 4, cnt = nbw & 15;
-    for (int e = 0; e < cnt; ++e) {
-      const int idx = bv.nb_items[first + e];
-      full |= test_sphere(lgeo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
-    }
-    cs.spheres += cnt;
-    trapped = fix && !full && bi == hint;
-    return true;
-  }
-  const unsigned ncand = rec.x & 0xFFFFu;
-  if (ncand != kCamOverflow) {  // every BVH sphere a ray of this pixel can hit is listed
+    items += nbw >> 4;
+    cnt = nbw & 15;
+  } else if (cam) {  // every BVH sphere a ray of this pixel can hit is listed
     clk.util(kUCam);
-    uint64_t lo = rec.x | (uint64_t)rec.y << 32, hi = rec.z | (uint64_t)rec.w << 32;
-    for (unsigned e = 0; e < ncand; ++e) {
+    cnt = (int)ncand;
+  } else {
+    clk.util(kUGrid);
+    const int cell = grid_locate(bv, ox, oy, oz, dx, dy, dz, bt);
+    listed = cell != kGridNone;
+    if (cell >= 0) {
+      const int e0 = bv.cell_start[cell];
+      items = bv.cell_items + e0;
+      cnt = bv.cell_start[cell + 1] - e0;
+    }
+  }
+  for (int e = 0; e < cnt; ++e) {
+    int idx;
+    if (cam) {
       lo = (lo >> 16) | (hi << 48);
       hi >>= 16;
-      const int idx = (int)(lo & 0xFFFFu);
-      test_sphere(lgeo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
+      idx = (int)(lo & 0xFFFFu);
+    } else {
+      idx = items[e];
     }
-    cs.spheres += ncand;
-    return true;
+    if (idx == hint) continue;
+    full |= test_sphere(lgeo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
   }
-  clk.util(kUGrid);
-  const bool done =
-      grid_point_query(lgeo, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs.spheres, full);
+  cs.spheres += cnt;
   clk.mark(kSecQGrid);
-  if (done) {
+  if (listed) {
     trapped = fix && !full && bi == hint;
     return true;
   }
@@ -516,6 +522,10 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
 #define PSRT_LDS_LEAVES 1  // leaf index + sphere reads from LDS in the walk
 #endif
 
+#ifndef PSRT_QDEPTH
+#define PSRT_QDEPTH 2  // look-ahead queue depth (accepted random_in_unit_sphere trials)
+#endif
+
 #ifndef PSRT_TRACE_WAVES
 #define PSRT_TRACE_WAVES 6  // min waves per SIMD requested from the register allocator
                             // (6: 80 VGPRs, +2% over 5 despite 4 spilled VGPRs; 7 loses)
@@ -590,6 +600,9 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   // look-ahead of random_in_unit_sphere (vec3.h:83-95): accepted trials, in
   // stream order, as raw rand() triples (z, y, x draw order)
   uint32_t q0x = 0, q0y = 0, q0z = 0, q1x = 0, q1y = 0, q1z = 0;
+#if PSRT_QDEPTH > 2
+  uint32_t q2x = 0, q2y = 0, q2z = 0;
+#endif
   int qn = 0;
   double pbt = 0.0;      // closest t / index so far of this ray's world.hit
   int pbi = -1;
@@ -742,7 +755,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       // take it (their stream advances), so the draws stay in stream order
       for (int f = 0;; ++f) {
         if (f >= a.rng_fill && __ballot(want && qn == 0) == 0) break;
-        const bool go = can_fill && qn < 2;
+        const bool go = can_fill && qn < PSRT_QDEPTH;
         if (go) clk.util(kUTrial);
         uint32_t z, y, x;
         uint64_t nxt;
@@ -754,6 +767,10 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
         const bool to0 = push && qn == 0, to1 = push && qn == 1;
         q0x = to0 ? x : q0x, q0y = to0 ? y : q0y, q0z = to0 ? z : q0z;
         q1x = to1 ? x : q1x, q1y = to1 ? y : q1y, q1z = to1 ? z : q1z;
+#if PSRT_QDEPTH > 2
+        const bool to2 = push && qn == 2;
+        q2x = to2 ? x : q2x, q2y = to2 ? y : q2y, q2z = to2 ? z : q2z;
+#endif
         qn += push ? 1 : 0;
       }
     }
@@ -766,6 +783,9 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       // vec3.h:78-81 random(-1, 1) from the queued draws; vec3.h:102-109 flip
       double rx = pm1_of(q0x), ry = pm1_of(q0y), rz = pm1_of(q0z);
       q0x = q1x, q0y = q1y, q0z = q1z;
+#if PSRT_QDEPTH > 2
+      q1x = q2x, q1y = q2y, q1z = q2z;
+#endif
       --qn;
       if (!((rx * h.nx + ry * h.ny) + rz * h.nz > 0.0)) rx = -rx, ry = -ry, rz = -rz;
       dx = ((h.px + h.nx) + rx) - h.px;
