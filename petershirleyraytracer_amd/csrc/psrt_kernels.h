@@ -31,6 +31,7 @@ struct TraceArgs {
   unsigned long long* stamps;       // diagnostic build: cycles per section (kSecCount)
   unsigned batch;                   // parked lanes that trigger a batched BVH pass
   int rng_fill;                     // look-ahead trials per lane per iteration (min)
+  int rng_extra;                    // extra trials while a scattering lane has none queued
   unsigned refill_min;              // idle lanes that trigger the finish + refill block
   FastDiv div_s, div_w;             // unit / s_count, q / width
 };

@@ -525,6 +525,7 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
 #ifndef PSRT_QDEPTH
 #define PSRT_QDEPTH 2  // look-ahead queue depth (accepted random_in_unit_sphere trials)
 #endif
+static_assert(PSRT_QDEPTH == 2 || PSRT_QDEPTH == 3, "queue slots q0..q2 exist");
 
 #ifndef PSRT_TRACE_WAVES
 #define PSRT_TRACE_WAVES 6  // min waves per SIMD requested from the register allocator
@@ -597,6 +598,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   unsigned rays = 0;
   int hint = -1;  // sphere the ray starts on (the previous hit), tested first
   bool pending = false;  // parked for the next batched BVH pass
+  bool sc_wait = false;  // hit resolved (pbi, pbt), scatter waits for a queued trial
   // look-ahead of random_in_unit_sphere (vec3.h:83-95): accepted trials, in
   // stream order, as raw rand() triples (z, y, x draw order)
   uint32_t q0x = 0, q0y = 0, q0z = 0, q1x = 0, q1y = 0, q1z = 0;
@@ -697,7 +699,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     // lanes wait (or nothing else can progress): the pass then runs at high
     // SIMD occupancy instead of once per iteration for a handful of lanes.
     bool resolved = false, finish = false;
-    if (active && !pending) {
+    if (active && !pending && !sc_wait) {
       if (a.max_depth < 0) {  // main.cc:36-37 at the first call: black, no trace
         finish = true;
       } else {
@@ -746,15 +748,18 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     // can be generated early, in stream order, and queued; a lane that ends its
     // sample just drops its queue (those draws would never have been made, and
     // no other sample's stream depends on them). Every live lane tops up its
-    // queue each iteration, converged; the loop runs longer only while a lane
-    // that scatters now has nothing queued.
+    // queue each iteration, converged; the loop runs at most rng_extra more
+    // trials while a lane that scatters now has nothing queued. A lane still
+    // without a trial then keeps its resolved hit and scatters in a later
+    // iteration (sc_wait): its draws stay in stream order either way.
+    const bool want = (resolved && !finish) || sc_wait;
     {
-      const bool want = resolved && !finish;
       const bool can_fill = active && !finish;
       // branch-free body: every lane computes a trial; only lanes with room
       // take it (their stream advances), so the draws stay in stream order
       for (int f = 0;; ++f) {
-        if (f >= a.rng_fill && __ballot(want && qn == 0) == 0) break;
+        if (f >= a.rng_fill && (f >= a.rng_fill + a.rng_extra || __ballot(want && qn == 0) == 0))
+          break;
         const bool go = can_fill && qn < PSRT_QDEPTH;
         if (go) clk.util(kUTrial);
         uint32_t z, y, x;
@@ -777,7 +782,8 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     clk.mark(kSecFillShade);
 
     // ---- scatter: target = (p + n) + random_in_hemisphere(n)  (main.cc:42-43) ----
-    if (resolved && !finish) {
+    sc_wait = want && qn == 0;
+    if (want && qn > 0) {
       clk.util(kUScatter);
       const HitRec h = hit_record_of(lgeo[hit], linv[hit], t, ox, oy, oz, dx, dy, dz);
       // vec3.h:78-81 random(-1, 1) from the queued draws; vec3.h:102-109 flip
