@@ -56,6 +56,11 @@ PEAK_HBM = 8.0e12
 OPS_PER_TEST = 23
 EXEC_OPS_PER_TEST = 18
 BOX_OPS_FP64_EQ = 7  # FP32 slab test: 6 FMA + 7 min/max + compare = 14 FP32 ops
+# FP64 ops per traced ray outside the sphere/box tests (estimate from the
+# kernel source): hit record 18 (ray.h:25-28, sphere.cc:34-36, hittable.h:14-18),
+# scatter 26 (vec3.h:102-109, main.cc:42-43, the new ray's A), look-ahead
+# trials 9 x 1.91 per scatter (vec3.h:83-95) ~ 17  ->  ~61
+SHADE_OPS_PER_RAY = 61
 
 
 def parse():
@@ -219,7 +224,7 @@ def main():
         if step >= args.warmup:
             kernel_ms.append(st["kernel_ms"])
             rays.append(st["rays"])
-            executed.append((st["tests_executed"], st["box_tests"]))
+            executed.append((st["tests_executed"], st["box_tests"], st["rays_traced"]))
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t0
@@ -238,11 +243,14 @@ def main():
         tests = rays_launch * n  # sphere::hit calls of the reference algorithm
         ex_tests = float(np.mean([e[0] for e in executed]))
         ex_boxes = float(np.mean([e[1] for e in executed]))
-        # Executed VALU work of psrt_trace, in FP64-op slots: 18 per exact
-        # sphere test (17 FP64 ops + compare: the reference's 23-op test with A
-        # hoisted per ray and r*r per sphere, identical values) and 7 per FP32
-        # box test (14 FP32 ops at twice the FP64 rate). frac is utilisation.
-        ex_ops = ex_tests * EXEC_OPS_PER_TEST + ex_boxes * BOX_OPS_FP64_EQ
+        ex_rays = float(np.mean([e[2] for e in executed]))
+        # Algorithmic FP64 work of psrt_trace as executed, in FP64-op slots: 18
+        # per exact sphere test (17 FP64 ops + compare: the reference's 23-op
+        # test with A hoisted per ray and r*r per sphere, identical values), 7
+        # per FP32 box test (14 FP32 ops at twice the FP64 rate) and ~61 per
+        # traced ray for the hit record, scatter and RNG trials.
+        ex_ops = (ex_tests * EXEC_OPS_PER_TEST + ex_boxes * BOX_OPS_FP64_EQ
+                  + ex_rays * SHADE_OPS_PER_RAY)
         achieved = ex_ops / (avg_ms * 1e-3)
         ref_equiv = tests * OPS_PER_TEST / (avg_ms * 1e-3)
         # algorithmic HBM bytes of one psrt_trace launch: each sample's colour
@@ -276,6 +284,7 @@ def main():
                 "kernel": "psrt_trace",
                 "avg_launch_ms": round(avg_ms, 3),
                 "rays_per_launch": int(rays_launch),
+                "rays_traced_per_launch": int(ex_rays),
                 "reference_sphere_tests_per_launch": int(tests),
                 "executed_sphere_tests_per_launch": int(ex_tests),
                 "executed_box_tests_per_launch": int(ex_boxes),
@@ -284,10 +293,14 @@ def main():
                 "reference_ops_per_test": OPS_PER_TEST,
                 "reference_equivalent_tflops": round(ref_equiv / 1e12, 4),
                 "culling": "off (linear sweep)" if (args.no_cull or ex_boxes == 0) else "bvh",
+                "shade_ops_per_traced_ray": SHADE_OPS_PER_RAY,
+                "fixpoint": not args.no_fixpoint,
                 "note": ("VALU-issue bound (FP64 non-FMA op peak 256 CU x 64 lanes x 2.4 GHz); "
-                         "achieved = executed sphere tests x 18 + box tests x 7 (FP64-op slots) "
-                         "/ avg psrt_trace launch; shading, RNG and traversal control not "
-                         "counted; reference_equivalent = rays x spheres x 23 / launch"),
+                         "achieved = (executed sphere tests x 18 + box tests x 7 + traced rays "
+                         "x 61) FP64-op slots / avg psrt_trace launch; integer RNG, traversal "
+                         "control and SIMT divergence not counted; rays_per_launch = the "
+                         "reference's rays, rays_traced = those not proven to end black "
+                         "(DESIGN.md 9); reference_equivalent = rays x spheres x 23 / launch"),
                 "hbm_algorithmic_bytes_per_launch": hbm_alg,
                 "hbm_frac": round(hbm_alg / (avg_ms * 1e-3) / PEAK_HBM, 6),
             },

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 /* ---- error codes ---------------------------------------------------------- */
 #define RT_OK 0
@@ -96,6 +96,9 @@ typedef struct {
   uint64_t box_tests;      /* FP32 BVH box tests the device ran              */
   double kernel_ms;        /* device time of the trace kernels (HIP events)  */
   double total_ms;         /* device time of the whole render                */
+  uint64_t rays_traced;    /* of `rays`, those the device traced; the rest
+                              are the rays of provably trapped paths, ended
+                              early with the same result     */
 } rt_stats;
 
 /* Number of rows a shard owns. */

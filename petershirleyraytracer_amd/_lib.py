@@ -43,7 +43,7 @@ class RtParams(C.Structure):
 class RtStats(C.Structure):
     _fields_ = [("samples", C.c_uint64), ("rays", C.c_uint64), ("sphere_tests", C.c_uint64),
                 ("tests_executed", C.c_uint64), ("box_tests", C.c_uint64),
-                ("kernel_ms", C.c_double), ("total_ms", C.c_double)]
+                ("kernel_ms", C.c_double), ("total_ms", C.c_double), ("rays_traced", C.c_uint64)]
 
 
 class RtError(RuntimeError):

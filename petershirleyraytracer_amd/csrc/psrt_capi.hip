@@ -513,7 +513,7 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   if (!c) return set_error(RT_E_INVALID, "rt_context_sync_stats: ctx is NULL");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipEventSynchronize(c->ev_all1));
-  unsigned long long cnt[3] = {0, 0, 0};
+  unsigned long long cnt[4] = {0, 0, 0, 0};
   HIP_TRY(hipMemcpy(cnt, c->d_counters + 1, sizeof cnt, hipMemcpyDeviceToHost));
   const unsigned long long rays = cnt[0];
   double kms = 0.0;
@@ -528,6 +528,7 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   c->last.sphere_tests = rays * (uint64_t)(c->n_last > 0 ? c->n_last : 0);
   c->last.tests_executed = cnt[1];
   c->last.box_tests = cnt[2];
+  c->last.rays_traced = cnt[3];
   c->last.kernel_ms = kms;
   c->last.total_ms = all;
   if (std::getenv("PSRT_STAMPS")) {

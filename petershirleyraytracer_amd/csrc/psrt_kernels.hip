@@ -609,6 +609,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   double pbt = 0.0;      // closest t / index so far of this ray's world.hit
   int pbi = -1;
   CullStats cs{0u, 0u};
+  unsigned long long traced = 0;  // wave-uniform: rays this wave traced
   SectionClock<kStamps> clk;
   clk.start();
 
@@ -699,6 +700,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     // lanes wait (or nothing else can progress): the pass then runs at high
     // SIMD occupancy instead of once per iteration for a handful of lanes.
     bool resolved = false, finish = false;
+    traced += (unsigned)__popcll(__ballot(active && !pending && !sc_wait && a.max_depth >= 0));
     if (active && !pending && !sc_wait) {
       if (a.max_depth < 0) {  // main.cc:36-37 at the first call: black, no trace
         finish = true;
@@ -836,6 +838,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     if (wr) atomicAdd(a.ray_counter, wr);
     if (ws) atomicAdd(a.ray_counter + 1, ws);
     if (wb) atomicAdd(a.ray_counter + 2, wb);
+    if (traced) atomicAdd(a.ray_counter + 3, traced);
   }
 }
 

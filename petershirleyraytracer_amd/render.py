@@ -147,7 +147,7 @@ def save_scene(path: str, spheres, camera=None, **render_args) -> None:
 def stats_dict(s: RtStats) -> dict:
     return dict(samples=s.samples, rays=s.rays, sphere_tests=s.sphere_tests,
                 tests_executed=s.tests_executed, box_tests=s.box_tests,
-                kernel_ms=s.kernel_ms, total_ms=s.total_ms)
+                kernel_ms=s.kernel_ms, total_ms=s.total_ms, rays_traced=s.rays_traced)
 
 
 def render(spheres, camera, width: int, height: int, spp: int, max_depth: int = 50,

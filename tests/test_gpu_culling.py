@@ -124,6 +124,7 @@ def test_trapped_termination_is_bit_identical(oracle_mod, final_scene):
     assert np.array_equal(bits(a), bits(b)) and np.array_equal(ra, rb)
     assert sa["rays"] == sb["rays"]
     assert sa["tests_executed"] < sb["tests_executed"] / 2, (sa, sb)
+    assert sb["rays_traced"] == sb["rays"] and sa["rays_traced"] < sa["rays"] / 3, (sa, sb)
     want, _, rays = oracle_mod.render(final_scene, cam, 160, 90, 8, threads=8)
     assert np.array_equal(bits(a), bits(want)) and sa["rays"] == rays
 
