@@ -124,7 +124,7 @@ struct Builder {
     // cost model: traversal 1, intersection 2 (fp64 test ~ 2 fp32 box tests)
     const double leaf_cost = 2.0 * count;
     const double split_cost = 1.0 + 2.0 * best / std::max(bounds.area(), 1e-300);
-    if (count <= 4 && leaf_cost <= split_cost) return -1;
+    if (count <= PSRT_LEAF_SAH_MAX && leaf_cost <= split_cost) return -1;
     auto mid = std::partition(prims.begin() + b, prims.begin() + e,
                               [&](const Prim& p) { return bin_of(p) < best_k; });
     int m = (int)(mid - prims.begin());
@@ -196,7 +196,7 @@ BvhHost build_bvh(const rt_sphere* s, int n) {
   for (const Prim& p : prims) all.grow(p.box);
   double ext = 0.0;
   for (int k = 0; k < 3; ++k) ext = std::max(ext, all.hi[k] - all.lo[k]);
-  double cell = std::max(2.5 * median, ext / 128.0);
+  double cell = std::max(PSRT_GRID_CELL * median, ext / 128.0);
   if (!(cell > 0)) cell = std::max(ext, 1.0);
   GridHost& g = out.grid;
   g.finv = (float)(1.0 / cell);

@@ -31,7 +31,16 @@ static_assert(sizeof(BvhNode) == 32, "node layout");
 
 constexpr int kBvhMinSpheres = 17;   // below this the linear sweep wins
 constexpr double kBigRatio = 16.0;   // radius > 16 x median -> tested every ray
-constexpr int kLeafMax = 2;
+#ifndef PSRT_LEAF_MAX
+#define PSRT_LEAF_MAX 2
+#endif
+#ifndef PSRT_LEAF_SAH_MAX
+#define PSRT_LEAF_SAH_MAX 4  // SAH may stop splitting at this many spheres
+#endif
+#ifndef PSRT_GRID_CELL
+#define PSRT_GRID_CELL 2.5  // grid cell edge in median radii
+#endif
+constexpr int kLeafMax = PSRT_LEAF_MAX;
 constexpr int kNbMax = 15;           // neighbour lists longer than this use the grid
 
 // Point-location grid over the same padded boxes: cell -> spheres whose padded

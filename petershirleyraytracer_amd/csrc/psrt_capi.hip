@@ -418,6 +418,8 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     const char* r = std::getenv("PSRT_REFILL_MIN");  // tuning knob (default 16 of 64 lanes)
     ta.refill_min = r ? (unsigned)std::atoi(r) : 16u;
     if (ta.refill_min < 1) ta.refill_min = 1;
+    const char* wt = std::getenv("PSRT_WALK_TAIL");  // tuning knob (default 4 lanes)
+    ta.walk_tail = wt ? (unsigned)std::atoi(wt) : 4u;
   }
   const bool use_bvh = c->bvh && !(p->flags & RT_FLAG_NO_CULL);
   psrt::BvhView bv = bvh_view(c);

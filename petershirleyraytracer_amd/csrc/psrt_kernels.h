@@ -33,6 +33,7 @@ struct TraceArgs {
   int rng_fill;                     // look-ahead trials per lane per iteration (min)
   int rng_extra;                    // extra trials while a scattering lane has none queued
   unsigned refill_min;              // idle lanes that trigger the finish + refill block
+  unsigned walk_tail;               // a BVH pass stops once this few lanes still walk
   FastDiv div_s, div_w;             // unit / s_count, q / width
 };
 

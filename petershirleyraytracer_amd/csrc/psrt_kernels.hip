@@ -434,7 +434,7 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
                                              const double4* __restrict__ lgeo, int hint,
                                              double ox, double oy, double oz, double dx, double dy,
                                              double dz, double A, double& bt, int& bi,
-                                             CullStats& cs) {
+                                             CullStats& cs, int& node, unsigned tail) {
   // Far origins are re-based at their root-box entry o' = o + t0 d (FP64), so
   // the FP32 slab test sees |o'| <= the scene scale and its error bound holds;
   // box intervals are then tested over [-t0, bt - t0]. The exact sphere tests
@@ -448,14 +448,16 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
   const float oix = fox * ix, oiy = foy * iy, oiz = foz * iz;
   const float tlo = -(float)t0 * 1.00000048f;  // <= -t0: the ray's t >= 0
   float tmax = tmax_up(bt - t0);
-  int node = 0;
-  if constexpr (kDiag) ++cs.trav_rays;
+  if constexpr (kDiag) cs.trav_rays += node == 0;
   // Two nodes per trip: in DFS skip-link order an interior hit always
   // continues at node+1, so node+1 is loaded alongside node and, when node is
   // an interior hit, box-tested in the same trip; the trip then advances two
   // levels. Node n_nodes is a padding
   // node (psrt_bvh.cpp), so node+1 is always readable.
   while (node < bv.n_nodes) {
+    // tail cut: once no more than `tail` lanes still walk, they stop and keep
+    // their node; they resume in the next pass with the newly parked rays
+    if (tail && (unsigned)__popcll(__ballot(1)) <= tail) break;
     if constexpr (kDiag) {
       if (first_active_lane()) ++cs.wave_trips;
     }
@@ -512,8 +514,11 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
   SectionClock<false> noclk;
   if (!hit_quick(geo, geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs, noclk, trapped,
                  0u, bv.nb_word))
+  {
+    int node = 0;
     hit_traverse<false, false>(bv, bv.nodes, bv.leaf_idx, geo, hint, ox, oy, oz, dx, dy, dz, A,
-                               bt, bi, cs);
+                               bt, bi, cs, node, 0u);
+  }
   best_t = bt;
   return bi;
 }
@@ -598,6 +603,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   unsigned rays = 0;
   int hint = -1;  // sphere the ray starts on (the previous hit), tested first
   bool pending = false;  // parked for the next batched BVH pass
+  int wnode = 0;         // where the parked ray's walk resumes
   bool sc_wait = false;  // hit resolved (pbi, pbt), scatter waits for a queued trial
   // look-ahead of random_in_unit_sphere (vec3.h:83-95): accepted trials, in
   // stream order, as raw rand() triples (z, y, x draw order)
@@ -712,6 +718,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
           resolved = hit_quick(geo, lgeo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi,
                                cs, clk, trapped, q, lnb);
           pending = !resolved;
+          wnode = 0;
           if (trapped && k < a.max_depth) {
             // the reference traces the max_depth - k rays that remain, all at
             // t = +-0 on this sphere, then returns black (pbi >= 0 below)
@@ -733,9 +740,12 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
         if (pending) {
           clk.util(kUWalk);
           hit_traverse<kStamps, kLds && PSRT_LDS_LEAVES>(bv, nodes, lleaf, lgeo, hint, ox, oy,
-                                                         oz, dx, dy, dz, A, pbt, pbi, cs);
-          pending = false;
-          resolved = true;
+                                                         oz, dx, dy, dz, A, pbt, pbi, cs, wnode,
+                                                         movable ? a.walk_tail : 0u);
+          if (wnode >= bv.n_nodes) {
+            pending = false;
+            resolved = true;
+          }
         }
       }
     }
