@@ -108,16 +108,30 @@ __device__ __forceinline__ double half_pow(double x, int k) {
 // reference, so the result is the same. Ties go to the later index
 // (sphere.cc:26 accepts t == tmax). NaN follows the reference: a NaN
 // discriminant is not "< 0" and a NaN root passes both range tests.
+// With kFix (the small-scene trace path), it also decides the trapped-path
+// test of §9 on the way: C == 0 on the hint sphere, and every other sphere
+// clear of the origin (the direction-free part of test_sphere's pre-reject).
+template <bool kFix = false>
 __device__ __forceinline__ int sweep_linear(const double4* __restrict__ geo, int n, double ox,
                                             double oy, double oz, double dx, double dy, double dz,
-                                            double A, double tmin, double tmax, double& best_t) {
+                                            double A, double tmin, double tmax, double& best_t,
+                                            int hint = -1, bool* trapped = nullptr) {
   int best_i = -1;
   double closest = tmax;
+  bool fix = false, clear = true;
   for (int i = 0; i < n; ++i) {
     const double4 s = geo[i];
     const double ax = ox - s.x, ay = oy - s.y, az = oz - s.z;
     const double hb = (dx * ax + dy * ay) + dz * az;
     const double c = ((ax * ax + ay * ay) + az * az) - s.w;
+    if constexpr (kFix) {
+      if (i == hint) {
+        fix = c == 0.0 && s.w >= 0x1p-700 && s.w <= 0x1p700;
+      } else {
+        const double k2 = 2.0 * (c + 2.0 * s.w);
+        clear = clear && c > 0.0 && c * c >= 0x1p-34 * (c + s.w) * k2;
+      }
+    }
     const double disc = hb * hb - A * c;
     if (!(disc < 0.0)) {
       const double sq = __builtin_sqrt(disc);
@@ -134,6 +148,7 @@ __device__ __forceinline__ int sweep_linear(const double4* __restrict__ geo, int
     }
   }
   best_t = closest;
+  if constexpr (kFix) *trapped = fix && clear && best_i == hint;
   return best_i;
 }
 
@@ -726,9 +741,18 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
             finish = true;
           }
         } else {
-          pbi = sweep_linear(geo, a.n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), pbt);
+          // small scenes (no BVH): the reference scan, plus the §9 test
+          bool trapped = false;
+          pbi = sweep_linear<true>(geo, a.n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(),
+                                   pbt, bv.fixpoint ? hint : -1, &trapped);
           cs.spheres += a.n;
           resolved = true;
+          const double am = __builtin_fmax(__builtin_fabs(ox),
+                                           __builtin_fmax(__builtin_fabs(oy), __builtin_fabs(oz)));
+          if (trapped && am <= 0x1p40 && A > 0.0 && A < 1e200 && k < a.max_depth) {
+            rays += (unsigned)(a.max_depth - k);
+            finish = true;
+          }
         }
       }
     }
