@@ -467,38 +467,50 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
   // Two nodes per trip: in DFS skip-link order an interior hit always
   // continues at node+1, so node+1 is loaded alongside node and, when node is
   // an interior hit, box-tested in the same trip; the trip then advances two
-  // levels. Node n_nodes is a padding
-  // node (psrt_bvh.cpp), so node+1 is always readable.
-  while (node < bv.n_nodes) {
+  // levels. Node n_nodes is a padding node (psrt_bvh.cpp), so node+1 is
+  // always readable.
+  //
+  // While-while (Aila & Laine 2009): a lane that reaches a leaf stops and
+  // holds it while the other lanes keep walking; the held leaves are then
+  // tested together, so one pass of FP64 sphere tests serves every lane
+  // that has a leaf instead of one pass per trip in which any lane has one.
+  // A lane holding a leaf does not walk on, so its tmax is never stale.
+  int leaf = -1;
+  for (;;) {
     // tail cut: once no more than `tail` lanes still walk, they stop and keep
     // their node; they resume in the next pass with the newly parked rays
-    if (tail && (unsigned)__popcll(__ballot(1)) <= tail) break;
-    if constexpr (kDiag) {
-      if (first_active_lane()) ++cs.wave_trips;
+    const uint64_t walking = __ballot(node < bv.n_nodes);
+    if (walking == 0 || (tail && (unsigned)__popcll(walking) <= tail)) break;
+    while (node < bv.n_nodes && leaf < 0) {
+      if (tail && (unsigned)__popcll(__ballot(1)) <= tail) break;  // test the held leaves
+      if constexpr (kDiag) {
+        if (first_active_lane()) ++cs.wave_trips;
+      }
+      const float4 a0 = nodes[2 * node], a1 = nodes[2 * node + 1];
+      const float4 b0 = nodes[2 * node + 2], b1 = nodes[2 * node + 3];
+      // slab distances; FP32 FMA is fine here: the test only needs to be
+      // conservative, and the box padding covers its rounding (psrt_bvh.cpp).
+      // node+1's test runs only where node is an interior hit: the walk is
+      // VALU-issue bound, so skipping it beats overlapping it (measured).
+      const bool hit_a = slab_hit(a0, a1, ix, iy, iz, oix, oiy, oiz, tlo, tmax);
+      const int leaf_a = __float_as_int(a1.w), leaf_b = __float_as_int(b1.w);
+      int next;
+      if (!hit_a) {
+        next = __float_as_int(a0.w);
+      } else if (leaf_a >= 0) {
+        leaf = leaf_a;
+        next = __float_as_int(a0.w);
+      } else if (!slab_hit(b0, b1, ix, iy, iz, oix, oiy, oiz, tlo, tmax)) {
+        next = __float_as_int(b0.w);
+      } else if (leaf_b >= 0) {
+        leaf = leaf_b;
+        next = __float_as_int(b0.w);
+      } else {
+        next = node + 2;
+      }
+      cs.boxes += 2;
+      node = next;
     }
-    const float4 a0 = nodes[2 * node], a1 = nodes[2 * node + 1];
-    const float4 b0 = nodes[2 * node + 2], b1 = nodes[2 * node + 3];
-    // slab distances; FP32 FMA is fine here: the test only needs to be
-    // conservative, and the box padding covers its rounding (psrt_bvh.cpp).
-    // node+1's test runs only where node is an interior hit: the walk is
-    // VALU-issue bound, so skipping it beats overlapping it (measured).
-    const bool hit_a = slab_hit(a0, a1, ix, iy, iz, oix, oiy, oiz, tlo, tmax);
-    const int leaf_a = __float_as_int(a1.w), leaf_b = __float_as_int(b1.w);
-    int next, leaf = -1;
-    if (!hit_a) {
-      next = __float_as_int(a0.w);
-    } else if (leaf_a >= 0) {
-      leaf = leaf_a;
-      next = __float_as_int(a0.w);
-    } else if (!slab_hit(b0, b1, ix, iy, iz, oix, oiy, oiz, tlo, tmax)) {
-      next = __float_as_int(b0.w);
-    } else if (leaf_b >= 0) {
-      leaf = leaf_b;
-      next = __float_as_int(b0.w);
-    } else {
-      next = node + 2;
-    }
-    cs.boxes += 2;
     if (leaf >= 0) {
       const int first = leaf >> 8, cnt = leaf & 255;
       if constexpr (kDiag) {
@@ -513,8 +525,8 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
         ++cs.spheres;
       }
       tmax = tmax_up(bt - t0);
+      leaf = -1;
     }
-    node = next;
   }
 }
 
