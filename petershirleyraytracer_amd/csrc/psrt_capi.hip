@@ -410,11 +410,10 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     if (ta.batch < 1) ta.batch = 1;
     const char* f = std::getenv("PSRT_RNG_FILL");  // tuning knob (default 2)
     ta.rng_fill = f ? std::atoi(f) : 2;
-    if (ta.rng_fill < 0) ta.rng_fill = 0;
+    if (ta.rng_fill < 1) ta.rng_fill = 1;
     const char* x = std::getenv("PSRT_RNG_EXTRA");  // tuning knob (default 1, then defer)
     ta.rng_extra = x ? std::atoi(x) : 1;
     if (ta.rng_extra < 0) ta.rng_extra = 0;
-    if (ta.rng_fill < 1 && ta.rng_extra < 1) ta.rng_extra = 1;  // progress guarantee
     const char* r = std::getenv("PSRT_REFILL_MIN");  // tuning knob (default 16 of 64 lanes)
     ta.refill_min = r ? (unsigned)std::atoi(r) : 16u;
     if (ta.refill_min < 1) ta.refill_min = 1;

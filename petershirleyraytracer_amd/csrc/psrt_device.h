@@ -68,4 +68,22 @@ __device__ __forceinline__ double pm1_of(uint32_t x) {
   return (double)(int)(2u * x - 0x80000000u) * 0x1p-31;
 }
 
+// random_in_unit_sphere's test (vec3.h:88): !(v.x*v.x + v.y*v.y + v.z*v.z > 1)
+// on v = random(-1, 1) from raw draws (x, y, z), decided exactly in integers.
+// With w = draw - 2^30, each coordinate is w * 2^-30 (pm1_of), so the exact
+// sum is S * 2^-60, S = wx^2 + wy^2 + wz^2 < 3 * 2^60 (int64). The reference's
+// FP64 sum (three rounded squares, two rounded adds) is within 2^-51 of it
+// near 1, so when |S - 2^60| > 2^10 the integer comparison gives the same
+// answer; in the band left (probability ~2^-49 per trial) the FP64 expression
+// itself decides.
+__device__ __forceinline__ bool in_unit_sphere(uint32_t x, uint32_t y, uint32_t z) {
+  const int64_t wx = (int32_t)(x - 0x40000000u), wy = (int32_t)(y - 0x40000000u),
+                wz = (int32_t)(z - 0x40000000u);
+  const int64_t S = (wx * wx + wy * wy) + wz * wz;
+  const int64_t dlt = S - (int64_t(1) << 60);
+  if (dlt > 1024 || dlt < -1024) return dlt < 0 || dlt == 0;  // S <= 2^60
+  const double rz = pm1_of(z), ry = pm1_of(y), rx = pm1_of(x);
+  return !((rx * rx + ry * ry) + rz * rz > 1.0);
+}
+
 }  // namespace psrt

@@ -554,6 +554,10 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
 #define PSRT_LDS_LEAVES 1  // leaf index + sphere reads from LDS in the walk
 #endif
 
+#ifndef PSRT_INT_SPHERE
+#define PSRT_INT_SPHERE 0  // random_in_unit_sphere's test in int64 (psrt_device.h); measured slower
+#endif
+
 #ifndef PSRT_QDEPTH
 #define PSRT_QDEPTH 2  // look-ahead queue depth (accepted random_in_unit_sphere trials)
 #endif
@@ -805,16 +809,19 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       const bool can_fill = active && !finish;
       // branch-free body: every lane computes a trial; only lanes with room
       // take it (their stream advances), so the draws stay in stream order
-      for (int f = 0;; ++f) {
-        if (f >= a.rng_fill && (f >= a.rng_fill + a.rng_extra || __ballot(want && qn == 0) == 0))
-          break;
+      int f = 0;
+      do {
         const bool go = can_fill && qn < PSRT_QDEPTH;
         if (go) clk.util(kUTrial);
         uint32_t z, y, x;
         uint64_t nxt;
         rand31_x3(rng, z, y, x, nxt);  // z, y, x: g++'s draw order (vec3.h:78-81)
+#if PSRT_INT_SPHERE
+        const bool in = in_unit_sphere(x, y, z);
+#else
         const double rz = pm1_of(z), ry = pm1_of(y), rx = pm1_of(x);
         const bool in = !((rx * rx + ry * ry) + rz * rz > 1.0);
+#endif
         rng = go ? nxt : rng;
         const bool push = go && in;
         const bool to0 = push && qn == 0, to1 = push && qn == 1;
@@ -825,7 +832,9 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
         q2x = to2 ? x : q2x, q2y = to2 ? y : q2y, q2z = to2 ? z : q2z;
 #endif
         qn += push ? 1 : 0;
-      }
+        ++f;
+      } while (f < a.rng_fill ||
+               (f < a.rng_fill + a.rng_extra && __ballot(want && qn == 0) != 0));
     }
     clk.mark(kSecFillShade);
 
