@@ -5,11 +5,12 @@
     torchrun --nproc-per-node N bench.py --gpus N ...        (N > 1, RCCL)
 
 A step is one full frame of the configured workload: every rank renders its
-interleaved rows (psrt_trace + psrt_reduce through rt_render_device, inputs
-resident in HBM), the FP64 framebuffer is gathered to rank 0 over RCCL and
-quantised there (write_color, color.h:8-24). Total work is fixed as N grows
-("strong" scaling). Rank 0 prints one JSON line; value = W*H*spp*K / wall,
-wall = max over ranks between barriers.
+interleaved rows (psrt_camera_lists + psrt_trace + psrt_reduce through
+rt_render_device, inputs resident in HBM) and quantises them (write_color,
+color.h:8-24, per pixel); the uint8 rows are gathered to rank 0 over RCCL
+(--gather-fp64: the FP64 accumulators, quantised on rank 0). Total work is
+fixed as N grows ("strong" scaling). Rank 0 prints one JSON line; value =
+W*H*spp*K / wall, wall = max over ranks between barriers.
 
 Default workload (BASELINE.json north star, configs[2]): the final
 random-spheres scene (485 spheres), 1200x800, 100 spp, depth 50.
@@ -77,6 +78,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--save-ppm", default="")
     ap.add_argument("--no-cull", action="store_true", help="force the linear sphere sweep")
+    ap.add_argument("--gather-fp64", action="store_true",
+                    help="N > 1: gather the FP64 accumulators and quantise on rank 0 "
+                         "(default: each rank quantises its rows, uint8 gather)")
     ap.add_argument("--no-fixpoint", action="store_true",
                     help="trace provably trapped paths to max_depth (DESIGN.md §9)")
     return ap.parse_args()
@@ -198,6 +202,7 @@ def main():
     dev = torch.device("cuda", local)
     acc = torch.zeros((rows, w, 3), dtype=torch.float64, device=dev)
     rgb = torch.zeros((h, w, 3), dtype=torch.uint8, device=dev) if rank == 0 else None
+    rgb_rows = torch.zeros((rows, w, 3), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
 
     def barrier():
@@ -214,12 +219,19 @@ def main():
         if world == 1:
             ctx.render_device(prm, acc.data_ptr(), rgb.data_ptr(), stream.cuda_stream)
             frame = gather_frame(acc, h, rank, world) if distributed else acc
-        else:
+        elif args.gather_fp64:
             ctx.render_device(prm, acc.data_ptr(), 0, stream.cuda_stream)
             frame = gather_frame(acc, h, rank, world)
             if rank == 0:
                 ctx.quantize_device(frame.data_ptr(), w, h, spp, rgb.data_ptr(),
                                     stream.cuda_stream)
+        else:
+            # write_color is per pixel: each rank quantises its own rows, and
+            # the gather moves 3 B per pixel instead of 24 (C3: 2.9 MB, not 23)
+            ctx.render_device(prm, acc.data_ptr(), rgb_rows.data_ptr(), stream.cuda_stream)
+            frame = gather_frame(rgb_rows, h, rank, world)
+            if rank == 0:
+                rgb.copy_(frame)
         st = ctx.sync_stats()
         if step >= args.warmup:
             kernel_ms.append(st["kernel_ms"])
@@ -273,7 +285,7 @@ def main():
             "data": "synthetic (procedural scene: final random-spheres, glibc srand(1); counter RNG seed 0)",
             "config": {"workload": cfg["desc"], "config_id": args.config, "width": w,
                        "height": h, "spp": spp, "max_depth": args.max_depth, "spheres": n,
-                       "parallelism": f"interleaved rows x{world}" + (", RCCL framebuffer gather" if world > 1 else "")},
+                       "parallelism": f"interleaved rows x{world}" + ((", RCCL FP64 framebuffer gather" if args.gather_fp64 else ", per-rank write_color + RCCL uint8 gather") if world > 1 else "")},
             "roofline": {
                 "bound": "valu",
                 "achieved": round(achieved / 1e12, 4),

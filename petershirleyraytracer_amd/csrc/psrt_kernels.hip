@@ -506,7 +506,21 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
         leaf = leaf_b;
         next = __float_as_int(b0.w);
       } else {
+#if PSRT_TRIP3
+        // node+1 is an interior hit too: its first child node+2 in this trip
+        const float4 c0 = nodes[2 * node + 4], c1 = nodes[2 * node + 5];
+        const int leaf_c = __float_as_int(c1.w);
+        if (!slab_hit(c0, c1, ix, iy, iz, oix, oiy, oiz, tlo, tmax)) {
+          next = __float_as_int(c0.w);
+        } else if (leaf_c >= 0) {
+          leaf = leaf_c;
+          next = __float_as_int(c0.w);
+        } else {
+          next = node + 3;
+        }
+#else
         next = node + 2;
+#endif
       }
       cs.boxes += 2;
       node = next;
@@ -556,6 +570,10 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
 
 #ifndef PSRT_INT_SPHERE
 #define PSRT_INT_SPHERE 0  // random_in_unit_sphere's test in int64 (psrt_device.h); measured slower
+#endif
+
+#ifndef PSRT_TRIP3
+#define PSRT_TRIP3 0  // BVH trips descend up to three levels
 #endif
 
 #ifndef PSRT_QDEPTH

@@ -34,13 +34,17 @@ def _worker(rank, world, port, w, h, spp, out_path):
     off, stride = shard(rank, world)
     sph = O.scene_random_spheres(1)
     cam = O.camera_look_at(aspect=w / h)
-    acc, _, _ = O.render(sph, cam, w, h, spp, 50, 0, off, stride)
+    acc, rgb, _ = O.render(sph, cam, w, h, spp, 50, 0, off, stride)
     assert acc.shape[0] == rows_owned(h, rank, world)
     frame = gather_frame(torch.from_numpy(acc), h, rank, world)
+    # bench.py's default N > 1 step: each rank quantises its rows (write_color
+    # is per pixel) and only the uint8 rows are gathered
+    frame8 = gather_frame(torch.from_numpy(np.ascontiguousarray(rgb)), h, rank, world)
     if rank == 0:
         np.save(out_path, frame.numpy())
+        np.save(out_path + ".rgb.npy", frame8.numpy())
     else:
-        assert frame is None
+        assert frame is None and frame8 is None
     dist.barrier()
     dist.destroy_process_group()
 
@@ -58,6 +62,8 @@ def test_gather_interleaved_rows(tmp_path, world, h):
     got = np.load(out)
     assert got.shape == want.shape
     assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+    got8 = np.load(out + ".rgb.npy")
+    assert got8.dtype == np.uint8 and np.array_equal(got8, O.quantize(want, spp))
 
 
 def test_shard_math():
