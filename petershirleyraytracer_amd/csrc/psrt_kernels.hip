@@ -24,6 +24,10 @@
 #include "psrt_device.h"
 #include "psrt_kernels.h"
 
+#ifndef PSRT_SLAB_ASM
+#define PSRT_SLAB_ASM 1  // slab test min/max as inline asm (no per-box NaN canonicalisation)
+#endif
+
 namespace psrt {
 
 __device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
@@ -276,8 +280,24 @@ __device__ __forceinline__ bool slab_hit(const float4 lo, const float4 hi, float
   const float x0 = __builtin_fmaf(lo.x, ix, -oix), x1 = __builtin_fmaf(hi.x, ix, -oix);
   const float y0 = __builtin_fmaf(lo.y, iy, -oiy), y1 = __builtin_fmaf(hi.y, iy, -oiy);
   const float z0 = __builtin_fmaf(lo.z, iz, -oiz), z1 = __builtin_fmaf(hi.z, iz, -oiz);
+#if PSRT_SLAB_ASM
+  // v_min3/v_max3 directly: no NaN canonicalisation of tlo / tmax per box
+  // (NaN cannot occur: finite boxes, safe_inv directions, finite tmax)
+  float tn, tf, a, b;
+  asm("v_min_f32 %0, %1, %2" : "=v"(a) : "v"(x0), "v"(x1));
+  asm("v_min_f32 %0, %1, %2" : "=v"(b) : "v"(y0), "v"(y1));
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(tn) : "v"(a), "v"(b), "v"(tlo));
+  asm("v_min_f32 %0, %1, %2" : "=v"(a) : "v"(z0), "v"(z1));
+  asm("v_max_f32 %0, %1, %2" : "=v"(tn) : "v"(tn), "v"(a));
+  asm("v_max_f32 %0, %1, %2" : "=v"(a) : "v"(x0), "v"(x1));
+  asm("v_max_f32 %0, %1, %2" : "=v"(b) : "v"(y0), "v"(y1));
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(tf) : "v"(a), "v"(b), "v"(tmax));
+  asm("v_max_f32 %0, %1, %2" : "=v"(a) : "v"(z0), "v"(z1));
+  asm("v_min_f32 %0, %1, %2" : "=v"(tf) : "v"(tf), "v"(a));
+#else
   const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tlo));
   const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tmax));
+#endif
   return tn <= tf;
 }
 
