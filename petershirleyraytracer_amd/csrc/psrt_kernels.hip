@@ -237,7 +237,28 @@ __device__ __forceinline__ bool test_sphere(const double4 s, int idx, double ox,
 // cannot be bounded this way (the BVH must be walked).
 constexpr int kGridNone = -1, kGridOutside = -2;
 
-__device__ __forceinline__ int grid_locate(const BvhView& bv, double ox, double oy, double oz,
+// The uniform constants hit_quick / the walk read on every ray. psrt_trace
+// keeps them in LDS and re-reads them per use (an LDS read issues on the LDS
+// pipe); held in SGPRs across the loop they spill, and each reload from the
+// spill lane is a VALU v_readlane (~20 per grid query).
+struct GridC {
+  float glo[3], ghi[3], ginv, gmargin;
+  int gdims[3], pad_;
+  double r_check, nb_c2;
+};
+
+__device__ __forceinline__ GridC grid_consts(const BvhView& bv) {
+  GridC g;
+  for (int k = 0; k < 3; ++k) g.glo[k] = bv.glo[k], g.ghi[k] = bv.ghi[k], g.gdims[k] = bv.gdims[k];
+  g.ginv = bv.ginv;
+  g.gmargin = bv.gmargin;
+  g.pad_ = 0;
+  g.r_check = bv.r_check;
+  g.nb_c2 = bv.nb_c2;
+  return g;
+}
+
+__device__ __forceinline__ int grid_locate(const GridC& bv, double ox, double oy, double oz,
                                            double dx, double dy, double dz, double bt) {
   if (!(bt < 1e30)) return kGridNone;
   // FP32 is enough: the test is conservative and its error (~2^-22 of the
@@ -340,7 +361,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
                                           double oz, double dx, double dy, double dz, double A,
                                           double& bt, int& bi, CullStats& cs, Clock& clk,
                                           bool& trapped, unsigned q,
-                                          const int* __restrict__ lnb) {
+                                          const int* __restrict__ lnb, const GridC& gc) {
   bt = __builtin_inf();
   bi = -1;
   trapped = false;
@@ -370,8 +391,8 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     // to ~2^-19 S) stays in that ball. A sphere with an accepted root t <= bt
     // has its hit point there and within the root error of its own surface,
     // so its centre lies within r_j + r_k + pad of c_j: it is j's neighbour.
-    if (bi == hint && am <= bv.r_check && bv.nb_c2 >= 0.0 &&
-        (ch <= 0.0 || ch * ch <= bv.nb_c2 * sh.w))
+    if (bi == hint && am <= gc.r_check && gc.nb_c2 >= 0.0 &&
+        (ch <= 0.0 || ch * ch <= gc.nb_c2 * sh.w))
       nbw = lnb[hint];
   }
   clk.mark(kSecQHint);
@@ -401,7 +422,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     cnt = (int)ncand;
   } else {
     clk.util(kUGrid);
-    const int cell = grid_locate(bv, ox, oy, oz, dx, dy, dz, bt);
+    const int cell = grid_locate(gc, ox, oy, oz, dx, dy, dz, bt);
     listed = cell != kGridNone;
     if (cell >= 0) {
       const int e0 = bv.cell_start[cell];
@@ -427,7 +448,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     trapped = fix && !full && bi == hint;
     return true;
   }
-  if (!(am <= bv.r_check)) {
+  if (!(am <= gc.r_check)) {
     // Far origin (e.g. inside the r=1000 ground): test [0, bt] against the
     // padded root box in FP64 (error ~1e-13 relative, far inside the pad). A
     // miss proves no BVH sphere can have a root in [0, bt]; a hit parks the
@@ -573,8 +594,9 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
   int bi;
   bool trapped;
   SectionClock<false> noclk;
+  const GridC gc = grid_consts(bv);
   if (!hit_quick(geo, geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs, noclk, trapped,
-                 0u, bv.nb_word))
+                 0u, bv.nb_word, gc))
   {
     int node = 0;
     hit_traverse<false, false>(bv, bv.nodes, bv.leaf_idx, geo, hint, ox, oy, oz, dx, dy, dz, A,
@@ -628,6 +650,8 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   // refill through an offset the compiler cannot see through: held across
   // the loop they would take ~40 registers and spill to scratch.
   __shared__ RefillConst s_rc;
+  __shared__ GridC s_gc;
+  if (threadIdx.x == 0) s_gc = grid_consts(bv);
   if (threadIdx.x < 12)
     s_rc.cam[threadIdx.x] = threadIdx.x < 3   ? a.org[threadIdx.x]
                             : threadIdx.x < 6 ? a.llc[threadIdx.x - 3]
@@ -784,8 +808,11 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
         clk.util(kUHit);
         if constexpr (kBVH) {
           bool trapped;
+          unsigned zg = 0;
+          asm volatile("" : "+v"(zg));  // re-read the grid constants from LDS here
+          const GridC& gc = *(const GridC*)((const char*)&s_gc + zg);
           resolved = hit_quick(geo, lgeo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi,
-                               cs, clk, trapped, q, lnb);
+                               cs, clk, trapped, q, lnb, gc);
           pending = !resolved;
           wnode = 0;
           if (trapped && k < a.max_depth) {
