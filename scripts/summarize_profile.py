@@ -42,6 +42,15 @@ avg = {}
 for line in csv.DictReader(open(stats)):
     if "psrt_trace" in line["Name"]:
         avg = dict(calls=int(line["Calls"]), average_ns=float(line["AverageNs"]))
+# per-dispatch durations: the first launch is bench.py's warmup step, which
+# bench.py's own HIP-event average leaves out; report the timed launches too
+trace = os.path.join(src, "trace", "run_kernel_trace.csv")
+if os.path.exists(trace):
+    d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+         for r in csv.DictReader(open(trace)) if "psrt_trace" in r["Kernel_Name"]]
+    if len(d) > 1:
+        avg["average_ns_after_warmup"] = sum(d[1:]) / len(d[1:])
+    avg["dispatch_ns"] = d
 fetch = c.get("FETCH_SIZE", 0.0) * 1024 * 2
 write = c.get("WRITE_SIZE", 0.0) * 1024
 secs = avg.get("average_ns", 0) * 1e-9
