@@ -24,6 +24,11 @@
 #include "psrt_device.h"
 #include "psrt_kernels.h"
 
+#ifndef PSRT_ABLATE
+#define PSRT_ABLATE 0  // measurement builds: 1 = hit_quick twice, 2 = two trials per trial,
+                       // 3 = the BVH walk twice
+#endif
+
 #ifndef PSRT_SLAB_ASM
 #define PSRT_SLAB_ASM 1  // slab test min/max as inline asm (no per-box NaN canonicalisation)
 #endif
@@ -709,6 +714,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   int pbi = -1;
   CullStats cs{0u, 0u};
   unsigned long long traced = 0;  // wave-uniform: rays this wave traced
+  unsigned ablate_sink = 0;       // PSRT_ABLATE measurement builds only
   SectionClock<kStamps> clk;
   clk.start();
 
@@ -811,6 +817,18 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
           unsigned zg = 0;
           asm volatile("" : "+v"(zg));  // re-read the grid constants from LDS here
           const GridC& gc = *(const GridC*)((const char*)&s_gc + zg);
+#if PSRT_ABLATE == 1  // measurement only: the section runs twice, the copy's result sunk
+          {
+            double x0 = ox, x1 = oy, x2 = oz, x3 = dx, x4 = dy, x5 = dz, bt2;
+            asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4), "+v"(x5));
+            int bi2;
+            bool tr2;
+            CullStats cs2{0u, 0u};
+            const bool r2 = hit_quick(geo, lgeo, a.n, bv, hint, x0, x1, x2, x3, x4, x5, A, bt2,
+                                      bi2, cs2, clk, tr2, q, lnb, gc);
+            ablate_sink += (unsigned)bi2 + (unsigned)r2 + (unsigned)tr2 + (unsigned)(bt2 > 1.0);
+          }
+#endif
           resolved = hit_quick(geo, lgeo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi,
                                cs, clk, trapped, q, lnb, gc);
           pending = !resolved;
@@ -844,6 +862,18 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       if (pend != 0 && ((unsigned)__popcll(pend) >= a.batch || movable == 0)) {
         if (pending) {
           clk.util(kUWalk);
+#if PSRT_ABLATE == 3  // measurement only: the walk runs twice, the copy's result sunk
+          {
+            double x0 = ox, bt2 = pbt;
+            int bi2 = pbi, n2 = wnode;
+            asm volatile("" : "+v"(x0), "+v"(n2));
+            CullStats cs2{0u, 0u};
+            hit_traverse<false, kLds && PSRT_LDS_LEAVES>(bv, nodes, lleaf, lgeo, hint, x0, oy,
+                                                         oz, dx, dy, dz, A, bt2, bi2, cs2, n2,
+                                                         movable ? a.walk_tail : 0u);
+            ablate_sink += (unsigned)bi2 + (unsigned)n2 + (unsigned)(bt2 > 1.0);
+          }
+#endif
           hit_traverse<kStamps, kLds && PSRT_LDS_LEAVES>(bv, nodes, lleaf, lgeo, hint, ox, oy,
                                                          oz, dx, dy, dz, A, pbt, pbi, cs, wnode,
                                                          movable ? a.walk_tail : 0u);
@@ -881,6 +911,17 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
         uint32_t z, y, x;
         uint64_t nxt;
         rand31_x3(rng, z, y, x, nxt);  // z, y, x: g++'s draw order (vec3.h:78-81)
+#if PSRT_ABLATE == 2  // measurement only: a second trial computed and sunk
+        {
+          uint64_t r2 = rng ^ 0x9E3779B97F4A7C15ULL;
+          asm volatile("" : "+v"(r2));
+          uint32_t z2, y2, x2;
+          uint64_t n2;
+          rand31_x3(r2, z2, y2, x2, n2);
+          const double a2 = pm1_of(z2), b2 = pm1_of(y2), c2 = pm1_of(x2);
+          ablate_sink += (unsigned)!((c2 * c2 + b2 * b2) + a2 * a2 > 1.0) + (unsigned)n2;
+        }
+#endif
 #if PSRT_INT_SPHERE
         const bool in = in_unit_sphere(x, y, z);
 #else
@@ -947,6 +988,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     }
   }
 
+  if (PSRT_ABLATE && ablate_sink == 0x9E3779B9u && a.width < 0) samples[0] = ablate_sink;
   // rays / sphere tests / box tests of this wave -> one atomic each
   unsigned long long wr = rays, ws = cs.spheres, wb = cs.boxes;
   for (int off = 32; off > 0; off >>= 1) {
