@@ -83,6 +83,10 @@ def parse():
                          "(default: each rank quantises its rows, uint8 gather)")
     ap.add_argument("--no-fixpoint", action="store_true",
                     help="trace provably trapped paths to max_depth (DESIGN.md §9)")
+    ap.add_argument("--emulate-shard", default="",
+                    help="R/G: one process renders only rank R's rows of a G-GPU run "
+                         "(per-rank step time of the multi-GPU bench, on one GPU; "
+                         "no gather, no CPU baseline)")
     return ap.parse_args()
 
 
@@ -194,8 +198,16 @@ def main():
     spheres, cam = scene_of(cfg)
     ctx = P.Context(local)
     ctx.set_scene(spheres, cam)
-    off, stride = shard(rank, world)
-    rows = rows_owned(h, rank, world)
+    if args.emulate_shard:
+        if world != 1:
+            raise SystemExit("--emulate-shard runs in a single process")
+        er, eg = (int(x) for x in args.emulate_shard.split("/"))
+        off, stride = shard(er, eg)
+        rows = rows_owned(h, er, eg)
+        args.no_cpu_baseline = True
+    else:
+        off, stride = shard(rank, world)
+        rows = rows_owned(h, rank, world)
     prm = P.params(w, h, spp, args.max_depth, args.seed, off, stride,
                    (FLAG_NO_CULL if args.no_cull else 0)
                    | (FLAG_NO_FIXPOINT if args.no_fixpoint else 0))
@@ -245,7 +257,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    total_samples = w * h * spp * args.steps
+    # an emulated shard processed only its own rows
+    total_samples = (rows if args.emulate_shard else h) * w * spp * args.steps
     value = total_samples / elapsed / 1e6
 
     if rank == 0:
@@ -285,7 +298,8 @@ def main():
             "data": "synthetic (procedural scene: final random-spheres, glibc srand(1); counter RNG seed 0)",
             "config": {"workload": cfg["desc"], "config_id": args.config, "width": w,
                        "height": h, "spp": spp, "max_depth": args.max_depth, "spheres": n,
-                       "parallelism": f"interleaved rows x{world}" + ((", RCCL FP64 framebuffer gather" if args.gather_fp64 else ", per-rank write_color + RCCL uint8 gather") if world > 1 else "")},
+                       "parallelism": (f"emulated shard {args.emulate_shard} (rows {off}::{stride})"
+                                       if args.emulate_shard else f"interleaved rows x{world}") + ((", RCCL FP64 framebuffer gather" if args.gather_fp64 else ", per-rank write_color + RCCL uint8 gather") if world > 1 else "")},
             "roofline": {
                 "bound": "valu",
                 "achieved": round(achieved / 1e12, 4),

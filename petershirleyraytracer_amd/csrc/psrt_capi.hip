@@ -6,6 +6,7 @@
 // psrt_trace megakernel launch and one psrt_reduce launch on a HIP stream.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -108,6 +109,8 @@ struct rt_context {
   size_t accum_tmp_cap = 0;  // doubles
   uint4* d_plist = nullptr;  // camera-ray candidate lists, one uint4 per owned pixel
   size_t plist_cap = 0;      // records
+  unsigned long long* d_wave_log = nullptr;  // diagnostic (PSRT_STAMPS): per-wave timeline
+  size_t wave_log_cap = 0, wave_log_used = 0;
   unsigned long long* d_counters = nullptr;  // [0] queue head, [1] rays, [2] tests, [3] boxes
   std::vector<hipEvent_t> ev;  // pairs around each trace launch
   int ev_used = 0;
@@ -205,6 +208,7 @@ int rt_context_destroy(rt_context* c) {
   (void)hipFree(c->d_samples);
   (void)hipFree(c->d_accum_tmp);
   (void)hipFree(c->d_plist);
+  (void)hipFree(c->d_wave_log);
   (void)hipFree(c->d_counters);
   (void)hipFree(c->d_nodes);
   (void)hipFree(c->d_leaf_geo);
@@ -353,6 +357,46 @@ static int check_params(const rt_params* p) {
   return RT_OK;
 }
 
+// Guided work queue (psrt_kernels.h TraceArgs::ph_*). The first ticket size
+// is the power of two <= total / (D x resident waves), clamped to [64, 1024]:
+// a window takes ~77 loop iterations per 1024 units, so on a small launch (a
+// strong-scaled shard) a 1024-unit window of expensive pixels would outlast
+// the rest of the launch. Working back from the end of the queue, each later
+// phase halves the size (down to 64) and holds about K tickets per resident
+// wave. Ticket ranges are contiguous: units a phase cannot fill with whole
+// tickets carry into the next one. PSRT_QUEUE_D / PSRT_QUEUE_K: tuning knobs.
+static void queue_phases(psrt::TraceArgs& ta, int grid) {
+  const char* ek = std::getenv("PSRT_QUEUE_K");
+  const char* ed = std::getenv("PSRT_QUEUE_D");
+  const double k = ek ? std::atof(ek) : 1.0;
+  const double d = ed ? std::atof(ed) : 8.0;
+  const uint64_t waves = (uint64_t)grid * (psrt::kTraceBlock / 64);
+  unsigned s0 = psrt::kWorkChunk;
+  while (s0 > 64 && (double)ta.total_units < d * (double)waves * (double)s0) s0 >>= 1;
+  unsigned size[psrt::kQueuePhases];
+  for (int p = 0; p < psrt::kQueuePhases; ++p) size[p] = std::max(64u, s0 >> p);
+  uint64_t alloc[psrt::kQueuePhases], rem = ta.total_units;
+  for (int p = psrt::kQueuePhases - 1; p >= 1; --p) {
+    const uint64_t want = size[p] < size[p - 1]
+                              ? (uint64_t)(k * (double)waves * (double)size[p]) : 0;
+    alloc[p] = std::min(rem, want);
+    rem -= alloc[p];
+  }
+  alloc[0] = rem;
+  uint64_t first = 0, base = 0, carry = 0;
+  for (int p = 0; p < psrt::kQueuePhases; ++p) {
+    ta.ph_first[p] = first;
+    ta.ph_base[p] = base;
+    ta.ph_size[p] = size[p];
+    const uint64_t units = alloc[p] + carry;
+    const uint64_t n = units / size[p];
+    carry = units - n * size[p];
+    first += n;
+    base += n * size[p];
+  }
+  ta.ph_first[psrt::kQueuePhases] = ~0ull;
+}
+
 int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigned char* d_rgb8,
                      void* stream_) {
   if (!c) return set_error(RT_E_INVALID, "rt_render_device: ctx is NULL");
@@ -404,6 +448,20 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   HIP_TRY(hipMemsetAsync(c->d_counters + 1, 0, 63 * sizeof(unsigned long long), st));
   const bool stamps = std::getenv("PSRT_STAMPS") != nullptr;  // diagnostic build
   ta.stamps = c->d_counters + 8;
+  ta.wave_log = nullptr;
+  if (stamps) {
+    const size_t need = (size_t)std::max(c->grid, c->grid_bvh) * (psrt::kTraceBlock / 64) * 3;
+    if (c->wave_log_cap < need) {
+      (void)hipFree(c->d_wave_log);
+      c->d_wave_log = nullptr;
+      c->wave_log_cap = 0;
+      HIP_TRY(hipMalloc(&c->d_wave_log, need * sizeof(unsigned long long)));
+      c->wave_log_cap = need;
+    }
+    HIP_TRY(hipMemsetAsync(c->d_wave_log, 0, need * sizeof(unsigned long long), st));
+    ta.wave_log = c->d_wave_log;
+    c->wave_log_used = need / 3;
+  }
   {
     const char* e = std::getenv("PSRT_BATCH");  // tuning knob (default 24 of 64 lanes)
     ta.batch = e ? (unsigned)std::atoi(e) : 24u;
@@ -468,6 +526,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     ta.s_count = sc;
     ta.div_s = fast_div_make((unsigned)sc);
     ta.total_units = (uint64_t)P * sc;
+    queue_phases(ta, use_bvh ? c->grid_bvh : c->grid);
     HIP_TRY(hipMemsetAsync(c->d_counters, 0, sizeof(unsigned long long), st));
     HIP_TRY(hipEventRecord(c->ev[2 * ch], st));
     const double4* g4 = c->d_geo;
@@ -546,6 +605,40 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
       u += b;
     }
     std::fprintf(stderr, "%s}}\n", u.c_str());
+    if (c->d_wave_log && c->wave_log_used) {
+      // wave timeline of the last launch: start, queue-empty and exit times
+      // relative to the first start, percentiles over waves, in microseconds
+      std::vector<unsigned long long> wl(c->wave_log_used * 3);
+      HIP_TRY(hipMemcpy(wl.data(), c->d_wave_log, wl.size() * sizeof(unsigned long long),
+                        hipMemcpyDeviceToHost));
+      unsigned long long t0 = ~0ull;
+      for (size_t w = 0; w < c->wave_log_used; ++w)
+        if (wl[3 * w]) t0 = std::min(t0, wl[3 * w]);
+      std::vector<double> st_, ex, en;
+      for (size_t w = 0; w < c->wave_log_used; ++w) {
+        if (!wl[3 * w]) continue;
+        st_.push_back((wl[3 * w] - t0) * 0.01);
+        if (wl[3 * w + 1]) ex.push_back((wl[3 * w + 1] - t0) * 0.01);
+        en.push_back((wl[3 * w + 2] - t0) * 0.01);
+      }
+      auto pct = [](std::vector<double> v) {
+        std::string r = "[";
+        if (!v.empty()) {
+          std::sort(v.begin(), v.end());
+          const double q[6] = {0, 0.1, 0.5, 0.9, 0.99, 1.0};
+          for (int k = 0; k < 6; ++k) {
+            char b[32];
+            std::snprintf(b, sizeof b, "%s%.1f", k ? ", " : "", v[(size_t)(q[k] * (v.size() - 1))]);
+            r += b;
+          }
+        }
+        return r + "]";
+      };
+      std::fprintf(stderr,
+                   "{\"psrt_waves\": {\"waves\": %zu, \"pct\": [0, 10, 50, 90, 99, 100], "
+                   "\"start_us\": %s, \"queue_empty_us\": %s, \"exit_us\": %s}}\n",
+                   st_.size(), pct(st_).c_str(), pct(ex).c_str(), pct(en).c_str());
+    }
     double tot = 0;
     for (int k = 0; k < 8; ++k) tot += (double)sec[k];
     std::fprintf(stderr,

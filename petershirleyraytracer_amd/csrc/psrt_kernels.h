@@ -7,7 +7,8 @@
 namespace psrt {
 
 constexpr int kTraceBlock = 512;     // 8 waves per workgroup (3 per CU share 160 KB of LDS)
-constexpr unsigned kWorkChunk = 1024;  // units a wave takes per queue dequeue
+constexpr unsigned kWorkChunk = 512;   // largest queue ticket (units); see queue_phases
+constexpr int kQueuePhases = 5;        // guided: ticket sizes halve toward the end, >= 64
 constexpr int kLdsNodes = 640;         // BVH nodes staged per workgroup (20 KB of LDS)
 constexpr int kLdsSpheres = 640;       // spheres staged per workgroup (25 KB of LDS)
 
@@ -26,9 +27,18 @@ struct TraceArgs {
   int s_begin, s_count; // sample chunk [s_begin, s_begin + s_count)
   uint64_t total_units; // pixels * s_count  (< 2^32)
   uint64_t seedmix;     // splitmix64(seed)
-  unsigned long long* work_counter;
+  unsigned long long* work_counter;  // queue tickets taken (one atomicAdd of 1 per ticket)
+  // Guided work queue: tickets [ph_first[p], ph_first[p+1]) of phase p cover
+  // ph_size[p] units each from unit ph_base[p] on; the last phase is open.
+  // Sizes shrink toward the end of the queue, so the last windows are small
+  // and the waves finish together (host: queue_phases in psrt_capi.hip).
+  uint64_t ph_first[kQueuePhases + 1];
+  uint64_t ph_base[kQueuePhases];
+  unsigned ph_size[kQueuePhases];
   unsigned long long* ray_counter;  // [0] rays, [1] sphere tests, [2] box tests
   unsigned long long* stamps;       // diagnostic build: cycles per section (kSecCount)
+  unsigned long long* wave_log;     // diagnostic build: per wave {start, queue empty, exit}
+                                    // (s_memrealtime, 100 MHz), or nullptr
   unsigned batch;                   // parked lanes that trigger a batched BVH pass
   int rng_fill;                     // look-ahead trials per lane per iteration (min)
   int rng_extra;                    // extra trials while a scattering lane has none queued

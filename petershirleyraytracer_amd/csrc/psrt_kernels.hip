@@ -717,6 +717,14 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   unsigned ablate_sink = 0;       // PSRT_ABLATE measurement builds only
   SectionClock<kStamps> clk;
   clk.start();
+  unsigned long long* wlog = nullptr;  // diagnostic build: this wave's timeline
+  if constexpr (kStamps) {
+    if (a.wave_log) {
+      wlog = a.wave_log + 3 * (size_t)(blockIdx.x * (kTraceBlock / 64) + threadIdx.x / 64);
+      const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+      if (lane == 0) wlog[0] = t, wlog[1] = 0;
+    }
+  }
 
   for (;;) {
     // ---- finish + refill lanes whose sample ended (wavefront ballot compaction) ----
@@ -750,10 +758,20 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     if (run_block && !exhausted) {
       const unsigned cnt = (unsigned)__popcll(need_mask);
       const unsigned rank = mbcnt64(need_mask);
+      // Guided work queue (TraceArgs::ph_*): one atomicAdd per ticket; ticket
+      // sizes shrink from kWorkChunk to 64 over the last few windows per wave,
+      // so no wave starts a large window while the others are nearly done.
+      // Every size is >= 64, so one ticket always covers the overflow.
       uint64_t nb = 0;
+      unsigned wsize = kWorkChunk;
       if (cnt > win_left) {
-        if (lane == 0) nb = atomicAdd(a.work_counter, (unsigned long long)kWorkChunk);
-        nb = __shfl(nb, 0);
+        uint64_t tk = 0;
+        if (lane == 0) tk = atomicAdd(a.work_counter, 1ull);
+        tk = __shfl(tk, 0);
+        int ph = 0;
+        while (ph < kQueuePhases - 1 && tk >= a.ph_first[ph + 1]) ++ph;
+        nb = a.ph_base[ph] + (tk - a.ph_first[ph]) * a.ph_size[ph];
+        wsize = a.ph_size[ph];
       }
       if (need) {
         clk.util(kURefill);
@@ -789,12 +807,18 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       }
       if (cnt > win_left) {  // the new window serves the overflow
         win_base = nb + (cnt - win_left);
-        win_left = kWorkChunk - (cnt - win_left);
+        win_left = wsize - (cnt - win_left);
       } else {
         win_base += cnt;
         win_left -= cnt;
       }
-      if (win_base >= total) exhausted = true;
+      if (win_base >= total) {
+        exhausted = true;
+        if constexpr (kStamps) {
+          const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+          if (wlog && lane == 0) wlog[1] = t;
+        }
+      }
     }
     clk.mark(kSecRefill);
     if (__ballot(active) == 0) break;
@@ -975,6 +999,10 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     clk.mark(kSecFillShade);
   }
   if constexpr (kStamps) {
+    if (wlog) {
+      const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+      if (lane == 0) wlog[2] = t;
+    }
     if (lane == 0)
       for (int k2 = 0; k2 < kSecCount; ++k2) atomicAdd(a.stamps + k2, (unsigned long long)clk.acc[k2]);
     // wave-level counters live in whichever lane was first active: sum them all

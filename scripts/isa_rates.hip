@@ -57,6 +57,16 @@ __global__ void __launch_bounds__(512) bench(unsigned long long* cyc, double* si
         if constexpr (kOp == 16) asm volatile("v_cvt_f32_f64 %0, %1" : "=v"(f[c]) : "v"(d[c]));
         if constexpr (kOp == 17) asm volatile("v_min_f64 %0, %0, %1" : "+v"(d[c]) : "v"(dy));
         if constexpr (kOp == 18) asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(w[c]) : "v"(w[0]));
+        if constexpr (kOp == 19) asm volatile("v_lshlrev_b64 %0, 7, %0" : "+v"(w[c]));
+        if constexpr (kOp == 20) asm volatile("v_lshrrev_b64 %0, 9, %0" : "+v"(w[c]));
+        if constexpr (kOp == 21) asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(u[c]) : "v"(uy));
+        if constexpr (kOp == 22) asm volatile("v_lshl_add_u32 %0, %0, 2, %1" : "+v"(u[c]) : "v"(uy));
+        if constexpr (kOp == 23) asm volatile("v_xad_u32 %0, %0, %1, %1" : "+v"(u[c]) : "v"(uy));
+        if constexpr (kOp == 24) asm volatile("v_sqrt_f64 %0, %0" : "+v"(d[c]));
+        if constexpr (kOp == 25) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(u[c]) : "v"(uy));
+        if constexpr (kOp == 26) asm volatile("v_mad_u32_u24 %0, %0, %1, %1" : "+v"(u[c]) : "v"(uy));
+        if constexpr (kOp == 27) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(u[c]) : "v"(uy) : "vcc");
+        if constexpr (kOp == 28) asm volatile("v_cvt_f64_u32 %0, %1" : "=v"(d[c]) : "v"(u[c]));
       }
     }
   }
@@ -72,7 +82,10 @@ static const char* kNames[] = {"v_add_f64",    "v_mul_f64",     "v_fma_f64",    
                                "v_fma_f32",    "v_mul_lo_u32",  "v_mad_u64_u32", "v_rcp_f64",
                                "v_rsq_f64",    "v_cvt_f64_i32", "v_ldexp_f64",   "v_xor_b32",
                                "v_mul_hi_u32", "v_pk_fma_f32",  "v_div_fixup_f64", "v_cmp_gt_f64",
-                               "v_cvt_f32_f64", "v_min_f64",    "v_lshl_add_u64"};
+                               "v_cvt_f32_f64", "v_min_f64",    "v_lshl_add_u64",
+                               "v_lshlrev_b64", "v_lshrrev_b64", "v_alignbit_b32", "v_lshl_add_u32",
+                               "v_xad_u32",    "v_sqrt_f64",    "v_mul_u32_u24", "v_mad_u32_u24",
+                               "v_cndmask_b32", "v_cvt_f64_u32"};
 
 template <int kOp>
 void run(int cus, double* sink, unsigned long long* dcyc) {
@@ -114,7 +127,7 @@ int main() {
       hipMalloc(&dcyc, sizeof(unsigned long long)) != hipSuccess)
     return 1;
   run<0>(cus, sink, dcyc);  // warm-up (clocks)
-  run_all<0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18>(cus, sink, dcyc);
+  run_all<0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28>(cus, sink, dcyc);
   (void)hipFree(sink);
   (void)hipFree(dcyc);
   return 0;
