@@ -450,7 +450,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   ta.stamps = c->d_counters + 8;
   ta.wave_log = nullptr;
   if (stamps) {
-    const size_t need = (size_t)std::max(c->grid, c->grid_bvh) * (psrt::kTraceBlock / 64) * 3;
+    const size_t need = (size_t)std::max(c->grid, c->grid_bvh) * (psrt::kTraceBlock / 64) * 5;
     if (c->wave_log_cap < need) {
       (void)hipFree(c->d_wave_log);
       c->d_wave_log = nullptr;
@@ -460,7 +460,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     }
     HIP_TRY(hipMemsetAsync(c->d_wave_log, 0, need * sizeof(unsigned long long), st));
     ta.wave_log = c->d_wave_log;
-    c->wave_log_used = need / 3;
+    c->wave_log_used = need / 5;
   }
   {
     const char* e = std::getenv("PSRT_BATCH");  // tuning knob (default 24 of 64 lanes)
@@ -535,7 +535,10 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     const bool lds = c->n_nodes + 1 <= psrt::kLdsNodes && c->n <= psrt::kLdsSpheres &&
                      c->n_leaf <= psrt::kLdsSpheres &&
                      !std::getenv("PSRT_NO_LDS");
+    // PSRT_BLOCKS_PER_CU: measurement knob (occupancy sweep), default = resident max
+    const char* bpc = std::getenv("PSRT_BLOCKS_PER_CU");
     auto launch = [&](auto kern, int grid) {
+      if (bpc) grid = std::min(grid, std::max(1, c->cus * std::atoi(bpc)));
       hipLaunchKernelGGL(kern, dim3(grid), blk, 0, st, g4, ir, c->d_samples, ta, bv);
     };
     if (!use_bvh)
@@ -608,18 +611,23 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
     if (c->d_wave_log && c->wave_log_used) {
       // wave timeline of the last launch: start, queue-empty and exit times
       // relative to the first start, percentiles over waves, in microseconds
-      std::vector<unsigned long long> wl(c->wave_log_used * 3);
+      std::vector<unsigned long long> wl(c->wave_log_used * 5);
       HIP_TRY(hipMemcpy(wl.data(), c->d_wave_log, wl.size() * sizeof(unsigned long long),
                         hipMemcpyDeviceToHost));
       unsigned long long t0 = ~0ull;
       for (size_t w = 0; w < c->wave_log_used; ++w)
-        if (wl[3 * w]) t0 = std::min(t0, wl[3 * w]);
-      std::vector<double> st_, ex, en;
+        if (wl[5 * w]) t0 = std::min(t0, wl[5 * w]);
+      std::vector<double> st_, ex, en, it_ex, it_dr;
       for (size_t w = 0; w < c->wave_log_used; ++w) {
-        if (!wl[3 * w]) continue;
-        st_.push_back((wl[3 * w] - t0) * 0.01);
-        if (wl[3 * w + 1]) ex.push_back((wl[3 * w + 1] - t0) * 0.01);
-        en.push_back((wl[3 * w + 2] - t0) * 0.01);
+        const unsigned long long* e = &wl[5 * w];
+        if (!e[0]) continue;
+        st_.push_back((e[0] - t0) * 0.01);
+        if (e[1]) {
+          ex.push_back((e[1] - t0) * 0.01);
+          it_ex.push_back((double)e[3]);
+          it_dr.push_back((double)(e[4] - e[3]));
+        }
+        en.push_back((e[2] - t0) * 0.01);
       }
       auto pct = [](std::vector<double> v) {
         std::string r = "[";
@@ -636,8 +644,10 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
       };
       std::fprintf(stderr,
                    "{\"psrt_waves\": {\"waves\": %zu, \"pct\": [0, 10, 50, 90, 99, 100], "
-                   "\"start_us\": %s, \"queue_empty_us\": %s, \"exit_us\": %s}}\n",
-                   st_.size(), pct(st_).c_str(), pct(ex).c_str(), pct(en).c_str());
+                   "\"start_us\": %s, \"queue_empty_us\": %s, \"exit_us\": %s, "
+                   "\"iters_to_empty\": %s, \"drain_iters\": %s}}\n",
+                   st_.size(), pct(st_).c_str(), pct(ex).c_str(), pct(en).c_str(),
+                   pct(it_ex).c_str(), pct(it_dr).c_str());
     }
     double tot = 0;
     for (int k = 0; k < 8; ++k) tot += (double)sec[k];

@@ -37,8 +37,9 @@ struct TraceArgs {
   unsigned ph_size[kQueuePhases];
   unsigned long long* ray_counter;  // [0] rays, [1] sphere tests, [2] box tests
   unsigned long long* stamps;       // diagnostic build: cycles per section (kSecCount)
-  unsigned long long* wave_log;     // diagnostic build: per wave {start, queue empty, exit}
-                                    // (s_memrealtime, 100 MHz), or nullptr
+  unsigned long long* wave_log;     // diagnostic build: per wave {start, queue empty, exit,
+                                    // iterations at queue empty, at exit} (s_memrealtime,
+                                    // 100 MHz), or nullptr
   unsigned batch;                   // parked lanes that trigger a batched BVH pass
   int rng_fill;                     // look-ahead trials per lane per iteration (min)
   int rng_extra;                    // extra trials while a scattering lane has none queued

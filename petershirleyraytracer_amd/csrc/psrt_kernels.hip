@@ -718,9 +718,10 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   SectionClock<kStamps> clk;
   clk.start();
   unsigned long long* wlog = nullptr;  // diagnostic build: this wave's timeline
+  unsigned iters = 0;                   // diagnostic build: loop iterations of this wave
   if constexpr (kStamps) {
     if (a.wave_log) {
-      wlog = a.wave_log + 3 * (size_t)(blockIdx.x * (kTraceBlock / 64) + threadIdx.x / 64);
+      wlog = a.wave_log + 5 * (size_t)(blockIdx.x * (kTraceBlock / 64) + threadIdx.x / 64);
       const unsigned long long t = __builtin_amdgcn_s_memrealtime();
       if (lane == 0) wlog[0] = t, wlog[1] = 0;
     }
@@ -816,12 +817,13 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
         exhausted = true;
         if constexpr (kStamps) {
           const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-          if (wlog && lane == 0) wlog[1] = t;
+          if (wlog && lane == 0) wlog[1] = t, wlog[3] = iters;
         }
       }
     }
     clk.mark(kSecRefill);
     if (__ballot(active) == 0) break;
+    if constexpr (kStamps) ++iters;
 
     // ---- world.hit(r, 0, inf, rec)  (main.cc:40) ----
     // Cheap part for every live, non-parked lane; rays that need the BVH walk
@@ -1001,7 +1003,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   if constexpr (kStamps) {
     if (wlog) {
       const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-      if (lane == 0) wlog[2] = t;
+      if (lane == 0) wlog[2] = t, wlog[4] = iters;
     }
     if (lane == 0)
       for (int k2 = 0; k2 < kSecCount; ++k2) atomicAdd(a.stamps + k2, (unsigned long long)clk.acc[k2]);
