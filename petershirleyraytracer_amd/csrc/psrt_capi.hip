@@ -595,12 +595,14 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   c->last.kernel_ms = kms;
   c->last.total_ms = all;
   if (std::getenv("PSRT_STAMPS")) {
-    unsigned long long sec[32];
+    unsigned long long sec[48];
     HIP_TRY(hipMemcpy(sec, c->d_counters + 8, sizeof sec, hipMemcpyDeviceToHost));
-    static const char* names[10] = {"refill", "store", "hit", "hint", "nb", "cam",
-                                    "grid", "walk", "trial", "scatter"};
+    static const char* names[18] = {"refill", "store", "hit", "hint", "nb", "cam",
+                                    "grid", "walk", "trial", "scatter", "hint_hit",
+                                    "hint_tiny", "grid_cell", "grid_out", "grid_none_fin",
+                                    "grid_none_inf", "far_miss", "park"};
     std::string u = "{\"psrt_util\": {";
-    for (int k = 0; k < 10; ++k) {
+    for (int k = 0; k < 18; ++k) {
       char b[128];
       const double w = (double)sec[12 + 2 * k], l = (double)sec[13 + 2 * k];
       std::snprintf(b, sizeof b, "%s\"%s\": [%.4g, %.2f]", k ? ", " : "", names[k], w,

@@ -48,20 +48,25 @@ enum Section {
 // Lane utilisation probes (diagnostic build): per probe, wave executions and
 // active lanes, counted by the first active lane.
 enum Util { kURefill = 0, kUStore, kUHit, kUHint, kUNb, kUCam, kUGrid, kUWalk, kUTrial,
-            kUScatter, kUCount };
+            kUScatter,
+            // hit_quick outcomes (lanes per wave execution, counted where decided)
+            kUHintHit, kUHintTiny, kUGridCell, kUGridOut, kUGridNoneFin, kUGridNoneInf,
+            kUFarMiss, kUPark, kUCount };
 
 __device__ __forceinline__ bool first_active_lane();
 
 template <bool kOn>
 struct SectionClock {
   uint64_t t = 0, acc[kSecCount] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned uw[kOn ? kUCount : 1] = {}, ul[kOn ? kUCount : 1] = {};
+  // utilisation probes: {wave executions, active lanes} per probe, in the
+  // workgroup's LDS (LDS atomics by the first active lane); flushed at exit
+  unsigned* ucnt = nullptr;
   __device__ __forceinline__ void util(int u) {
     if constexpr (kOn) {
       const uint64_t m = __ballot(1);
       if (first_active_lane()) {
-        uw[u] += 1;
-        ul[u] += (unsigned)__popcll(m);
+        atomicAdd(ucnt + 2 * u, 1u);
+        atomicAdd(ucnt + 2 * u + 1, (unsigned)__popcll(m));
       }
     }
   }
@@ -390,6 +395,10 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     test_sphere(sh, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, &ch);
     fix = bv.fixpoint && ch == 0.0 && sh.w >= 0x1p-700 && sh.w <= 0x1p700 && am <= 0x1p40;
     ++cs.spheres;
+    if (bi == hint) {
+      clk.util(kUHintHit);
+      if (bt < 1e-6) clk.util(kUHintTiny);
+    }
     // Neighbour path: the hint sphere j was hit at bt and o
     // lies within pad/2 of its surface, so the segment [o, o + bt d] (both
     // ends in the ball of radius r_j + pad/2; the far end is a root of j, good
@@ -429,6 +438,10 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     clk.util(kUGrid);
     const int cell = grid_locate(gc, ox, oy, oz, dx, dy, dz, bt);
     listed = cell != kGridNone;
+    if (cell >= 0) clk.util(kUGridCell);
+    else if (cell == kGridOutside) clk.util(kUGridOut);
+    else if (bt < 1e30) clk.util(kUGridNoneFin);
+    else clk.util(kUGridNoneInf);
     if (cell >= 0) {
       const int e0 = bv.cell_start[cell];
       items = bv.cell_items + e0;
@@ -459,8 +472,12 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     // miss proves no BVH sphere can have a root in [0, bt]; a hit parks the
     // ray for the batched walk, which re-bases it at the box entry (hit_traverse).
     ++cs.boxes;
-    if (root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt) < 0.0) return true;
+    if (root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt) < 0.0) {
+      clk.util(kUFarMiss);
+      return true;
+    }
   }
+  clk.util(kUPark);
   return false;
 }
 
@@ -716,6 +733,12 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   unsigned long long traced = 0;  // wave-uniform: rays this wave traced
   unsigned ablate_sink = 0;       // PSRT_ABLATE measurement builds only
   SectionClock<kStamps> clk;
+  __shared__ unsigned s_util[kStamps ? 2 * kUCount : 1];
+  if constexpr (kStamps) {
+    for (int e = threadIdx.x; e < 2 * kUCount; e += blockDim.x) s_util[e] = 0u;
+    __syncthreads();
+    clk.ucnt = s_util;
+  }
   clk.start();
   unsigned long long* wlog = nullptr;  // diagnostic build: this wave's timeline
   unsigned iters = 0;                   // diagnostic build: loop iterations of this wave
@@ -1012,10 +1035,9 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     atomicAdd(a.stamps + 9, (unsigned long long)cs.wave_leaf_trips);
     atomicAdd(a.stamps + 10, (unsigned long long)cs.trav_rays);
     atomicAdd(a.stamps + 11, (unsigned long long)cs.leaf_visits);
-    for (int u = 0; u < kUCount; ++u) {
-      atomicAdd(a.stamps + 12 + 2 * u, (unsigned long long)clk.uw[u]);
-      atomicAdd(a.stamps + 13 + 2 * u, (unsigned long long)clk.ul[u]);
-    }
+    __syncthreads();  // every wave of the block has left the loop
+    for (int e = threadIdx.x; e < 2 * kUCount; e += blockDim.x)
+      atomicAdd(a.stamps + 12 + e, (unsigned long long)s_util[e]);
   }
 
   if (PSRT_ABLATE && ablate_sink == 0x9E3779B9u && a.width < 0) samples[0] = ablate_sink;
