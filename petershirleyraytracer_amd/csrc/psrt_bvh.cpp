@@ -225,12 +225,32 @@ BvhHost build_bvh(const rt_sphere* s, int n) {
       for (int y = c0[1]; y <= c1[1]; ++y)
         for (int x = c0[0]; x <= c1[0]; ++x) cells[cidx(x, y, z)].push_back(p.idx);
   }
-  g.start.resize(ncell + 1);
+  // lists [0, ncell): cells; [ncell, 2 ncell): 2x2x2 blocks, block b = the
+  // union of cells (x..x+1, y..y+1, z..z+1) of cell b's corner (clipped to the
+  // grid), for segments that cross at most one cell boundary per axis
+  g.start.resize(2 * ncell + 1);
   g.start[0] = 0;
   for (long c = 0; c < ncell; ++c) {
     g.start[c + 1] = g.start[c] + (int32_t)cells[c].size();
     g.items.insert(g.items.end(), cells[c].begin(), cells[c].end());
   }
+  std::vector<int32_t> blk;
+  for (int z = 0; z < g.dims[2]; ++z)
+    for (int y = 0; y < g.dims[1]; ++y)
+      for (int x = 0; x < g.dims[0]; ++x) {
+        blk.clear();
+        for (int dz = 0; dz <= 1 && z + dz < g.dims[2]; ++dz)
+          for (int dy = 0; dy <= 1 && y + dy < g.dims[1]; ++dy)
+            for (int dx = 0; dx <= 1 && x + dx < g.dims[0]; ++dx) {
+              const std::vector<int32_t>& cl = cells[cidx(x + dx, y + dy, z + dz)];
+              blk.insert(blk.end(), cl.begin(), cl.end());
+            }
+        std::sort(blk.begin(), blk.end());
+        blk.erase(std::unique(blk.begin(), blk.end()), blk.end());
+        const long b = ncell + cidx(x, y, z);
+        g.start[b + 1] = g.start[b] + (int32_t)blk.size();
+        g.items.insert(g.items.end(), blk.begin(), blk.end());
+      }
 
   // neighbour lists: two padded balls that meet have padded boxes that meet,
   // so both spheres share a cell (membership is conservative); candidates come

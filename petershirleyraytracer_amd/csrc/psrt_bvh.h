@@ -54,7 +54,10 @@ struct GridHost {
   float fhi[3] = {0, 0, 0};  // >= flo + dims/finv: the grid's outer bound
   float finv = 1.0f;
   int dims[3] = {0, 0, 0};
-  std::vector<int32_t> start;  // dims[0]*dims[1]*dims[2] + 1 offsets into items
+  // 2 x ncell + 1 offsets into items (ncell = dims[0]*dims[1]*dims[2]): list
+  // c < ncell is cell c; list ncell + c is the 2x2x2 block whose lowest cell
+  // is c (union of up to 8 cell lists, deduplicated)
+  std::vector<int32_t> start;
   std::vector<int32_t> items;  // original sphere indices
 };
 

@@ -116,6 +116,23 @@ __device__ __forceinline__ double half_pow(double x, int k) {
   return x;
 }
 
+// Root selection of sphere.cc:24-31 over [0, tmax], bit for bit, with one
+// division where the reference may take two: the near root t1 = n1/A
+// (n1 = -hb - sq) is certainly < 0, and not -0, when n1 < -A*2^-900 (also
+// when A*2^-900 underflows: then |n1/A| >= 2^-1074/A > 2^-952); the far root
+// then decides, as in the reference. If t1 > tmax the far root is rejected
+// too: -hb + sq >= -hb - sq after rounding and division by A > 0 is
+// monotone, so t2 >= t1. A second division runs only for t1 in (-2^-900, 0).
+// NaN roots pass, as in the reference. Returns whether the root t is taken.
+__device__ __forceinline__ bool root_select(double hb, double sq, double A, double tmax,
+                                            double& t) {
+  const double n1 = -hb - sq;
+  const bool far = n1 < -(A * 0x1p-900);
+  t = (far ? -hb + sq : n1) / A;
+  if (!far && t < 0.0) t = (-hb + sq) / A;
+  return !(t < 0.0 || t > tmax);
+}
+
 // Sphere sweep of hittable_list::hit(r, tmin, tmax, rec) (hittable_list.cc:3-20
 // over sphere.cc:3-33). Only the winner's record is formed afterwards
 // (hit_record_of): every earlier accepted record is overwritten in the
@@ -149,11 +166,16 @@ __device__ __forceinline__ int sweep_linear(const double4* __restrict__ geo, int
     const double disc = hb * hb - A * c;
     if (!(disc < 0.0)) {
       const double sq = __builtin_sqrt(disc);
-      double t = (-hb - sq) / A;
+      double t;
       bool ok = true;
-      if (t < tmin || t > closest) {
-        t = (-hb + sq) / A;
-        if (t < tmin || t > closest) ok = false;
+      if constexpr (kFix) {  // the trace path: tmin == 0
+        ok = root_select(hb, sq, A, closest, t);
+      } else {
+        t = (-hb - sq) / A;
+        if (t < tmin || t > closest) {
+          t = (-hb + sq) / A;
+          if (t < tmin || t > closest) ok = false;
+        }
       }
       if (ok) {
         closest = t;
@@ -228,11 +250,8 @@ __device__ __forceinline__ bool test_sphere(const double4 s, int idx, double ox,
   const double disc = hb * hb - A * c;
   if (disc < 0.0) return true;
   const double sq = __builtin_sqrt(disc);
-  double t = (-hb - sq) / A;
-  if (t < 0.0 || t > best_t) {
-    t = (-hb + sq) / A;
-    if (t < 0.0 || t > best_t) return true;
-  }
+  double t;
+  if (!root_select(hb, sq, A, best_t, t)) return true;
   if (t < best_t || idx > best_i) {  // equal t: the later index wins
     best_t = t;
     best_i = idx;
@@ -241,10 +260,11 @@ __device__ __forceinline__ bool test_sphere(const double4 s, int idx, double ox,
 }
 
 // Point query for a short segment [o, o + bt*d] (the common case: the ray
-// re-hit the sphere it starts on at t ~ 0). Returns the cell whose spheres
-// are the only BVH spheres the segment can hit, kGridOutside when the segment
-// lies outside the grid (no BVH sphere can be hit), or kGridNone when it
-// cannot be bounded this way (the BVH must be walked).
+// re-hit the sphere it starts on at t ~ 0). Returns the list (psrt_bvh.h
+// GridHost: a cell, or the 2x2x2 block of cells the segment crosses into)
+// whose spheres are the only BVH spheres the segment can hit, kGridOutside
+// when the segment lies outside the grid (no BVH sphere can be hit), or
+// kGridNone when it cannot be bounded this way (the BVH must be walked).
 constexpr int kGridNone = -1, kGridOutside = -2;
 
 // The uniform constants hit_quick / the walk read on every ray. psrt_trace
@@ -278,20 +298,28 @@ __device__ __forceinline__ int grid_locate(const GridC& bv, double ox, double oy
   const float d3[3] = {(float)dx, (float)dy, (float)dz};
   const float tb = (float)bt * 1.00000048f;
   int ci[3];
-  bool outside = false;
+  bool outside = false, ok = true, one = true;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const float e = __builtin_fmaf(tb, d3[k], o3[k]);
     const float lo = fminf(o3[k], e) - m, hi = fmaxf(o3[k], e) + m;
     const float glo = bv.glo[k], ghi = bv.ghi[k];
     if (hi < glo || lo > ghi) outside = true;
-    const int c0 = (int)__builtin_floorf((lo - glo) * bv.ginv);
-    const int c1 = (int)__builtin_floorf((hi - glo) * bv.ginv);
-    ci[k] = (c0 == c1 && c0 >= 0 && c0 < bv.gdims[k]) ? c0 : -1;
+    // cell range of the widened segment, clipped to the grid (in float, before
+    // the conversion: huge or NaN coordinates clip too): a hit point lies in a
+    // padded sphere box, hence in a cell of the grid
+    const float top = (float)(bv.gdims[k] - 1);
+    const int c0 = (int)fminf(fmaxf(__builtin_floorf((lo - glo) * bv.ginv), 0.0f), top);
+    const int c1 = (int)fminf(fmaxf(__builtin_floorf((hi - glo) * bv.ginv), 0.0f), top);
+    ok = ok && c1 - c0 <= 1;
+    one = one && c1 == c0;
+    ci[k] = c0;
   }
   if (outside) return kGridOutside;
-  if (ci[0] < 0 || ci[1] < 0 || ci[2] < 0) return kGridNone;
-  return (ci[2] * bv.gdims[1] + ci[1]) * bv.gdims[0] + ci[0];
+  if (!ok) return kGridNone;
+  // one cell: its list; two cells on some axis: the 2x2x2 block list from ci
+  const int cell = (ci[2] * bv.gdims[1] + ci[1]) * bv.gdims[0] + ci[0];
+  return one ? cell : cell + bv.gdims[0] * bv.gdims[1] * bv.gdims[2];
 }
 
 __device__ __forceinline__ float tmax_up(double t) {

@@ -1,5 +1,6 @@
 // Invariants of the exact-culling structures (psrt_bvh.cpp), checked on CPU.
 // Prints "ok <nodes> <big> <cells> <items>" or "FAIL <what>".
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -85,6 +86,26 @@ static void check_scene(const std::vector<rt_sphere>& s) {
           CHECK(found, "sphere listed in every touched cell");
         }
   }
+  // 2x2x2 block lists: list ncell + c = the deduplicated union of the cell
+  // lists of the (clipped) block whose lowest cell is c
+  const long ncell = (long)g.dims[0] * g.dims[1] * g.dims[2];
+  CHECK((long)g.start.size() == 2 * ncell + 1, "cell lists then block lists");
+  for (int z = 0; z < g.dims[2]; ++z)
+    for (int y = 0; y < g.dims[1]; ++y)
+      for (int x = 0; x < g.dims[0]; ++x) {
+        std::vector<int> want;
+        for (int dz = 0; dz <= 1 && z + dz < g.dims[2]; ++dz)
+          for (int dy = 0; dy <= 1 && y + dy < g.dims[1]; ++dy)
+            for (int dx = 0; dx <= 1 && x + dx < g.dims[0]; ++dx) {
+              const long cell = ((long)(z + dz) * g.dims[1] + y + dy) * g.dims[0] + x + dx;
+              for (int t = g.start[cell]; t < g.start[cell + 1]; ++t) want.push_back(g.items[t]);
+            }
+        std::sort(want.begin(), want.end());
+        want.erase(std::unique(want.begin(), want.end()), want.end());
+        const long bl = ncell + ((long)z * g.dims[1] + y) * g.dims[0] + x;
+        const std::vector<int> got(g.items.begin() + g.start[bl], g.items.begin() + g.start[bl + 1]);
+        CHECK(got == want, "block list = union of its cells");
+      }
   // neighbour lists: exactly the BVH spheres within |r_j| + |r_k| + 2 pad, or -1
   std::vector<char> big(n, 0);
   for (int i : b.big_idx) big[i] = 1;
@@ -110,7 +131,7 @@ static void check_scene(const std::vector<rt_sphere>& s) {
     for (int e = 0; e < (int)want.size(); ++e)
       CHECK(b.nb_items[(w >> 4) + e] == want[e], "neighbour list = all spheres in reach, sorted");
   }
-  std::printf("ok %d %zu %zu %zu\n", m, b.big_idx.size(), g.start.size() - 1, g.items.size());
+  std::printf("ok %d %zu %zu %zu\n", m, b.big_idx.size(), ncell, g.items.size());
 }
 
 int main() {
