@@ -158,18 +158,30 @@ def cpu_baseline(cfg, args, frame_acc):
     return cb, parity
 
 
-def traffic_from_profile(config: str):
-    """HBM bytes per psrt_trace launch from the committed rocprofv3 PMC
-    summary (profiles/pmc_<config>.json), FETCH_SIZE doubled per the gfx950
-    calibration note in MI355X_MICROARCH.md §HBM."""
+def profile_counters(config: str):
+    """From the committed rocprofv3 PMC summary (profiles/pmc_<config>.json):
+    HBM bytes per psrt_trace launch (FETCH_SIZE doubled per the gfx950
+    calibration note in MI355X_MICROARCH.md §HBM, + WRITE_SIZE) and the VALU
+    issue rate: SIMD cycles per wave64 VALU instruction, (kernel cycles x 1024
+    SIMDs) / SQ_INSTS_VALU, kernel cycles = GRBM_GUI_ACTIVE / 8 XCDs."""
     path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     try:
         d = json.load(open(path))
-        return float(d["hbm_bytes_per_launch"])
+        traffic = float(d["hbm_bytes_per_launch"])
     except Exception:
-        return None
+        return None, None
+    try:
+        c = d["counters"]
+        cycles = c["GRBM_GUI_ACTIVE"] / 8
+        valu = dict(insts_per_launch=c["SQ_INSTS_VALU"], kernel_cycles=cycles,
+                    simd_cycles_per_valu_inst=round(cycles * 1024 / c["SQ_INSTS_VALU"], 3),
+                    note="a wave64 FP64 VALU op holds a SIMD 4 cycles (16 lanes/cycle)",
+                    source=f"profiles/pmc_{config}.json")
+    except Exception:
+        valu = None
+    return traffic, valu
 
 
 def main():
@@ -282,7 +294,7 @@ def main():
         # written once (3 x 8 B); the 485 x 40 B sphere list is L2-resident
         samples_rank = rows * w * spp
         hbm_alg = samples_rank * 24
-        traffic = traffic_from_profile(args.config)
+        traffic, valu_issue = profile_counters(args.config)
         out = {
             "metric": METRIC,
             "value": round(value, 4),
@@ -329,6 +341,9 @@ def main():
                          "(DESIGN.md 9); reference_equivalent = rays x spheres x 23 / launch"),
                 "hbm_algorithmic_bytes_per_launch": hbm_alg,
                 "hbm_frac": round(hbm_alg / (avg_ms * 1e-3) / PEAK_HBM, 6),
+                # measured issue rate (PMC) of the same kernel: the SIMDs' VALU
+                # issue is the bound; frac above counts only the FP64 algorithm
+                "valu_issue": valu_issue,
             },
             "rays_per_sample": round(float(np.sum(rays)) / (rows * w * spp * args.steps), 3),
         }

@@ -357,27 +357,32 @@ static int check_params(const rt_params* p) {
   return RT_OK;
 }
 
-// Guided work queue (psrt_kernels.h TraceArgs::ph_*). The first ticket size
-// is the power of two <= total / (D x resident waves), clamped to [64, 1024]:
-// a window takes ~77 loop iterations per 1024 units, so on a small launch (a
-// strong-scaled shard) a 1024-unit window of expensive pixels would outlast
-// the rest of the launch. Working back from the end of the queue, each later
-// phase halves the size (down to 64) and holds about K tickets per resident
-// wave. Ticket ranges are contiguous: units a phase cannot fill with whole
-// tickets carry into the next one. PSRT_QUEUE_D / PSRT_QUEUE_K: tuning knobs.
-static void queue_phases(psrt::TraceArgs& ta, int grid) {
+// Guided work queue (psrt_kernels.h TraceArgs::ph_*), BVH scenes. The first
+// ticket size is the power of two <= total / (D x resident waves), clamped to
+// [64, kWorkChunk]: a window takes ~77 loop iterations per 1024 units, so on a
+// small launch (a strong-scaled shard) a large window of expensive pixels
+// would outlast the rest of the launch. Working back from the end of the
+// queue, each later phase halves the size (down to 64) and holds about K
+// tickets per resident wave. Ticket ranges are contiguous: units a phase
+// cannot fill with whole tickets carry into the next one. PSRT_QUEUE_D /
+// PSRT_QUEUE_K: tuning knobs.
+// Small scenes (the linear sweep, ~5x cheaper rays) keep fixed tickets of
+// kLinearChunk units: there the queue's atomics and the per-wave start-up
+// cost more than the launch tail (C1: 0.31 ms with 1024-unit tickets on a few
+// hundred waves vs 0.51 ms guided; C2 -7% guided).
+static void queue_phases(psrt::TraceArgs& ta, int grid, bool guided) {
   const char* ek = std::getenv("PSRT_QUEUE_K");
   const char* ed = std::getenv("PSRT_QUEUE_D");
   const double k = ek ? std::atof(ek) : 1.0;
   const double d = ed ? std::atof(ed) : 8.0;
   const uint64_t waves = (uint64_t)grid * (psrt::kTraceBlock / 64);
-  unsigned s0 = psrt::kWorkChunk;
-  while (s0 > 64 && (double)ta.total_units < d * (double)waves * (double)s0) s0 >>= 1;
+  unsigned s0 = guided ? psrt::kWorkChunk : psrt::kLinearChunk;
+  while (guided && s0 > 64 && (double)ta.total_units < d * (double)waves * (double)s0) s0 >>= 1;
   unsigned size[psrt::kQueuePhases];
-  for (int p = 0; p < psrt::kQueuePhases; ++p) size[p] = std::max(64u, s0 >> p);
+  for (int p = 0; p < psrt::kQueuePhases; ++p) size[p] = guided ? std::max(64u, s0 >> p) : s0;
   uint64_t alloc[psrt::kQueuePhases], rem = ta.total_units;
   for (int p = psrt::kQueuePhases - 1; p >= 1; --p) {
-    const uint64_t want = size[p] < size[p - 1]
+    const uint64_t want = guided && size[p] < size[p - 1]
                               ? (uint64_t)(k * (double)waves * (double)size[p]) : 0;
     alloc[p] = std::min(rem, want);
     rem -= alloc[p];
@@ -526,7 +531,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     ta.s_count = sc;
     ta.div_s = fast_div_make((unsigned)sc);
     ta.total_units = (uint64_t)P * sc;
-    queue_phases(ta, use_bvh ? c->grid_bvh : c->grid);
+    queue_phases(ta, use_bvh ? c->grid_bvh : c->grid, use_bvh);
     HIP_TRY(hipMemsetAsync(c->d_counters, 0, sizeof(unsigned long long), st));
     HIP_TRY(hipEventRecord(c->ev[2 * ch], st));
     const double4* g4 = c->d_geo;

@@ -7,7 +7,11 @@
 namespace psrt {
 
 constexpr int kTraceBlock = 512;     // 8 waves per workgroup (3 per CU share 160 KB of LDS)
-constexpr unsigned kWorkChunk = 512;   // largest queue ticket (units); see queue_phases
+#ifndef PSRT_WORK_CHUNK
+#define PSRT_WORK_CHUNK 512
+#endif
+constexpr unsigned kWorkChunk = PSRT_WORK_CHUNK;  // largest queue ticket (units); see queue_phases
+constexpr unsigned kLinearChunk = 1024;           // queue ticket of the small-scene (linear) path
 constexpr int kQueuePhases = 5;        // guided: ticket sizes halve toward the end, >= 64
 constexpr int kLdsNodes = 640;         // BVH nodes staged per workgroup (20 KB of LDS)
 constexpr int kLdsSpheres = 640;       // spheres staged per workgroup (25 KB of LDS)
