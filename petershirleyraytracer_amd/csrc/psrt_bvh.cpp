@@ -2,6 +2,7 @@
 #include "psrt_bvh.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <limits>
 
@@ -150,9 +151,11 @@ BvhHost build_bvh(const rt_sphere* s, int n) {
   std::vector<double> sorted = radii;
   std::nth_element(sorted.begin(), sorted.begin() + n / 2, sorted.end());
   const double median = sorted[n / 2];
+  const char* er = std::getenv("PSRT_BIG_RATIO");  // tuning knob
+  const double big_ratio = er ? std::atof(er) : kBigRatio;
   std::vector<Prim> prims;
   for (int i = 0; i < n; ++i) {
-    if (radii[i] > kBigRatio * median && radii[i] > 0) {
+    if (radii[i] > big_ratio * median && radii[i] > 0) {
       out.big_idx.push_back(i);
       continue;
     }

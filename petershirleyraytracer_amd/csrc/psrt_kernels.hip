@@ -291,8 +291,8 @@ __device__ __forceinline__ GridC grid_consts(const BvhView& bv) {
 __device__ __forceinline__ int grid_locate(const GridC& bv, double ox, double oy, double oz,
                                            double dx, double dy, double dz, double bt) {
   if (!(bt < 1e30)) return kGridNone;
-  // FP32 is enough: the test is conservative and its error (~2^-22 of the
-  // scene scale) is far inside the margin (pad/4, psrt_bvh.cpp)
+  // FP32 is enough within the caller's range guard: the test is conservative
+  // and its error is inside pad + margin (psrt_bvh.cpp, hit_quick)
   const float m = bv.gmargin;
   const float o3[3] = {(float)ox, (float)oy, (float)oz};
   const float d3[3] = {(float)dx, (float)dy, (float)dz};
@@ -464,7 +464,13 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     cnt = (int)ncand;
   } else {
     clk.util(kUGrid);
-    const int cell = grid_locate(gc, ox, oy, oz, dx, dy, dz, bt);
+    // FP32 query, exact while its error (~4 ulp of the segment's coordinates)
+    // stays below pad + margin = 1.25 pad (a hit point lies >= pad inside its
+    // sphere's padded box): coordinates up to ~630 S; admitted up to 256 S
+    // (|o| <= 4 r_check, bt |d| <= 4 r_check), else the walk / root-box test
+    const double rg = 4.0 * gc.r_check;
+    const int cell = (am <= rg && (bt * bt) * A <= rg * rg)
+                         ? grid_locate(gc, ox, oy, oz, dx, dy, dz, bt) : kGridNone;
     listed = cell != kGridNone;
     if (cell >= 0) clk.util(kUGridCell);
     else if (cell == kGridOutside) clk.util(kUGridOut);

@@ -100,6 +100,21 @@ def test_bvh_ties_and_degenerate_scenes():
         _compare(sph, o, rng.normal(size=(n, 3)))
 
 
+def test_far_origins_inside_a_huge_ground():
+    """Origins deep inside a ground sphere 10^4-10^5 scene scales big, aimed
+    at small spheres half sunk into its surface: the FP32 grid query is not
+    precise there, so these rays must take the guarded FP64 paths."""
+    rng = np.random.default_rng(17)
+    small = np.stack([rng.uniform(-3, 3, 300), rng.uniform(-0.2, 0.2, 300),
+                      rng.uniform(-3, 3, 300), rng.uniform(0.1, 0.4, 300)], 1)
+    sph = np.concatenate([[[0.0, -1e5, 0.0, 1e5]], small])
+    n = 100_000
+    depth = rng.choice([1e2, 1e3, 1e4, 1e5], n)
+    o = np.stack([rng.uniform(-3, 3, n), -depth, rng.uniform(-3, 3, n)], 1)
+    target = small[rng.integers(0, len(small), n), :3] + rng.normal(scale=0.2, size=(n, 3))
+    _compare(sph, o, target - o)
+
+
 def test_renders_cull_equals_no_cull(oracle_mod, final_scene):
     cam = P.camera_look_at(aspect=160 / 90)
     a, ra, sa = P.render(final_scene, cam, 160, 90, 8, cull=True)
