@@ -290,10 +290,10 @@ def main():
                   + ex_rays * SHADE_OPS_PER_RAY)
         achieved = ex_ops / (avg_ms * 1e-3)
         ref_equiv = tests * OPS_PER_TEST / (avg_ms * 1e-3)
-        # algorithmic HBM bytes of one psrt_trace launch: each sample's colour
-        # written once (3 x 8 B); the 485 x 40 B sphere list is L2-resident
+        # algorithmic HBM bytes of one psrt_trace launch: each sample's record
+        # (t: 8 B, k: 2 B) written once; the 485 x 40 B sphere list is L2-resident
         samples_rank = rows * w * spp
-        hbm_alg = samples_rank * 24
+        hbm_alg = samples_rank * 10
         traffic, valu_issue = profile_counters(args.config)
         out = {
             "metric": METRIC,

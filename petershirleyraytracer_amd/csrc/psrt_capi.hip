@@ -413,14 +413,20 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   const int rows = rt_rows_owned(p->height, p->row_offset, p->row_stride);
   const size_t P = (size_t)rows * p->width;
 
-  // sample chunking: samples buffer holds s_chunk x P x 3 doubles, units < 2^32
-  size_t s_chunk = sample_buffer_cap_bytes() / (P * 3 * sizeof(double));
+  // sample chunking: the samples buffer holds s_chunk x P records of
+  // kSampleBytes (t array, then k array), units < 2^32
+  // (chunks of a multiple of 4 samples where possible: psrt_reduce then reads
+  // 16-B aligned runs)
+  size_t s_chunk = sample_buffer_cap_bytes() / (P * psrt::kSampleBytes);
+  if (s_chunk > 4) s_chunk &= ~(size_t)3;
   if (s_chunk < 1) s_chunk = 1;
   if (s_chunk > (size_t)p->spp) s_chunk = p->spp;
   while (s_chunk > 1 && P * s_chunk >= (1ULL << 32)) s_chunk /= 2;
   if (P * s_chunk >= (1ULL << 32)) return set_error(RT_E_INVALID, "shard too large");
   const int nchunks = (int)((p->spp + s_chunk - 1) / s_chunk);
-  rc = ensure_buf(&c->d_samples, &c->samples_cap, s_chunk * P * 3);
+  // t array (doubles) then k array (uint16), P x s_chunk records each
+  const size_t recs = P * s_chunk;
+  rc = ensure_buf(&c->d_samples, &c->samples_cap, recs + (recs + 3) / 4);
   if (rc) return rc;
   double* acc = d_accum;
   if (!acc && nchunks > 1) {
@@ -558,15 +564,16 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[2 * ch + 1], st));
     psrt::ReduceArgs ra{};
-    ra.samples = c->d_samples;
+    ra.samp_t = c->d_samples;
+    ra.samp_k = (const unsigned short*)(c->d_samples + P * sc);  // after the t array
     ra.pixels = (unsigned)P;
     ra.s_count = sc;
     ra.first_chunk = ch == 0;
     ra.spp_total = p->spp;
     ra.accum = acc;
     ra.rgb8 = (ch == nchunks - 1) ? d_rgb8 : nullptr;
-    const unsigned blocks = (unsigned)((P + 255) / 256);
-    hipLaunchKernelGGL(psrt::psrt_reduce, dim3(blocks), dim3(256), 0, st, ra);
+    const unsigned blocks = (unsigned)((P + psrt::kReduceBlock - 1) / psrt::kReduceBlock);
+    hipLaunchKernelGGL(psrt::psrt_reduce, dim3(blocks), dim3(psrt::kReduceBlock), 0, st, ra);
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipEventRecord(c->ev_all1, st));

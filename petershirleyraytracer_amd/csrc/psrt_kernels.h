@@ -22,6 +22,16 @@ struct FastDiv {
   unsigned m, sh1, sh2, d;
 };
 
+// Sample record: t (double) and k (uint16); k = kSampleBlack for a black sample.
+constexpr unsigned short kSampleBlack = 0xFFFFu;
+constexpr int kSampleKCap = 1100;
+constexpr int kReduceBlock = 64;   // psrt_reduce: one wave per 64 pixels
+#ifndef PSRT_REDUCE_TILE
+#define PSRT_REDUCE_TILE 32
+#endif
+constexpr int kReduceTile = PSRT_REDUCE_TILE;  // (the loads assume 32)  // samples per pixel staged per LDS tile
+constexpr size_t kSampleBytes = sizeof(double) + sizeof(unsigned short);
+
 struct TraceArgs {
   int n;               // spheres (geo: {cx, cy, cz, r*r}, inv_r: 1.0/r)
   double org[3], llc[3], hor[3], ver[3];
@@ -91,7 +101,8 @@ struct CamListArgs {
 };
 
 struct ReduceArgs {
-  const double* samples;
+  const double* samp_t;           // [pixels][s_count] (unit order) sky parameter t (sample_colour)
+  const unsigned short* samp_k;   // [pixels][s_count] hits, or kSampleBlack
   unsigned pixels;
   int s_count;
   int first_chunk;

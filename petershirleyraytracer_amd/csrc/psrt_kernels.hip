@@ -15,7 +15,9 @@
 // Data layout in HBM:
 //   geo[n]      double4 {cx, cy, cz, r*r}   sphere.cc:11 radius*radius
 //   inv_r[n]    double  1.0/r              vec3.h:151-154 (1/t)*v
-//   samples     double[s_count][P][3]      colour of sample s of pixel q
+//   samples     double[P][s_count] t, uint16[P][s_count] k: sample s of pixel q at
+//               unit q*s_count + s (sample_colour)
+//                                          (sample_colour)
 //   accum       double[P][3]               P = rows_owned * W, reference order
 //   rgb8        uint8 [P][3]
 #include <hip/hip_runtime.h>
@@ -114,6 +116,22 @@ __device__ __forceinline__ double half_pow(double x, int k) {
   if (k <= 1000) return __builtin_ldexp(x, -k);
   for (int m = 0; m < k; ++m) x = 0.5 * x;
   return x;
+}
+
+// A sample's colour (main.cc:43-48): black, or the sky at t = 0.5 (y + 1)
+// (y: the last ray's unit direction) times 0.5^k, k = hits on the path. The
+// trace stores (t, k) and psrt_reduce forms the colour, with the same FP64
+// operations in the same order. k is stored capped at kSampleKCap: from
+// ~1076 halvings on, x <= 1 is +0 (and NaN stays NaN), so the cap changes no bit.
+__device__ __forceinline__ void sample_colour(double tt, unsigned short kk, double& r, double& g,
+                                              double& b) {
+  r = g = b = 0.0;
+  if (kk != kSampleBlack) {
+    const double w = 1.0 - tt;
+    r = half_pow(w + tt * 0.5, kk);
+    g = half_pow(w + tt * 0.7, kk);
+    b = half_pow(w + tt * 1.0, kk);
+  }
 }
 
 // Root selection of sphere.cc:24-31 over [0, tmax], bit for bit, with one
@@ -748,7 +766,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   int k = 0;          // bounces (hits) so far: current trace is at depth max_depth-k
   uint64_t rng = 0;
   unsigned q = 0;     // pixel index within the shard
-  unsigned sl = 0;    // sample index within the chunk
+  unsigned su = 0;    // this sample's unit (q * s_count + sample index in the chunk)
   unsigned rays = 0;
   int hint = -1;  // sphere the ray starts on (the previous hit), tested first
   bool pending = false;  // parked for the next batched BVH pass
@@ -796,20 +814,20 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     if (run_block) {
       // sky (main.cc:46-48) x 0.5^k, or black; store
       if (done) {
+        // The colour is a function of (t, k) alone (sample_colour): store those
+        // (10 B) in unit order. A wave's window is a run of consecutive units,
+        // so its stores fill whole lines in its XCD's L2 before write-back.
         clk.util(kUStore);
-        double col_r = 0.0, col_g = 0.0, col_b = 0.0;
+        double tt = 0.0;
+        unsigned short kk = kSampleBlack;
         if (pbi < 0 && a.max_depth >= 0) {
           const double y = (1.0 / __builtin_sqrt(A)) * dy;
-          const double tt = 0.5 * (y + 1.0);
-          const double w = 1.0 - tt;
-          col_r = half_pow(w + tt * 0.5, k);
-          col_g = half_pow(w + tt * 0.7, k);
-          col_b = half_pow(w + tt * 1.0, k);
+          tt = 0.5 * (y + 1.0);
+          kk = (unsigned short)(k < kSampleKCap ? k : kSampleKCap);
         }
-        double* dst = samples + ((size_t)sl * a.pixels + q) * 3;
-        dst[0] = col_r;
-        dst[1] = col_g;
-        dst[2] = col_b;
+        const unsigned u = su;  // < total < 2^32
+        samples[u] = tt;
+        ((unsigned short*)(samples + total))[u] = kk;  // k array follows the t array
         done = false;
       }
     }
@@ -840,7 +858,8 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
           const RefillConst& rc = *(const RefillConst*)((const char*)&s_rc + zo);
           const FastDiv ds = rc.div_s, dw = rc.div_w;
           q = fast_div((unsigned)unit, ds);
-          sl = (unsigned)unit - q * ds.d;
+          su = (unsigned)unit;
+          const unsigned sl = su - q * ds.d;
           const unsigned row_k = fast_div(q, dw);
           const unsigned i = q - row_k * dw.d;
           const int r = rc.row_offset + (int)row_k * rc.row_stride;
@@ -1104,22 +1123,85 @@ PSRT_INSTANTIATE(true, true, true)
 
 // pixel_color += sample, in sample order (main.cc:77-84); write_color on the
 // last chunk (color.h:8-24).
-__global__ __launch_bounds__(256) void psrt_reduce(ReduceArgs a) {
-  const unsigned q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= a.pixels) return;
+__global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
+  // One wave per 64 pixels. A pixel's samples are contiguous, so the wave
+  // stages [64 pixels][32 samples] tiles through LDS with 256-B runs per
+  // pixel, then each lane adds its pixel's samples in order.
+  __shared__ __attribute__((aligned(16))) double s_t[kReduceBlock][kReduceTile + 2];
+  __shared__ __attribute__((aligned(16))) unsigned short s_k[kReduceBlock][kReduceTile + 4];
+  const unsigned lane = threadIdx.x;
+  const unsigned q0 = blockIdx.x * kReduceBlock;
+  const unsigned q = q0 + lane;
+  const unsigned S = (unsigned)a.s_count;
   double r = 0.0, g = 0.0, b = 0.0;
-  if (!a.first_chunk) {
+  if (!a.first_chunk && q < a.pixels) {
     r = a.accum[(size_t)q * 3 + 0];
     g = a.accum[(size_t)q * 3 + 1];
     b = a.accum[(size_t)q * 3 + 2];
   }
-  const double* src = a.samples + (size_t)q * 3;
-  const size_t stride = (size_t)a.pixels * 3;
-  for (int s = 0; s < a.s_count; ++s, src += stride) {
-    r += src[0];
-    g += src[1];
-    b += src[2];
+  for (unsigned s0 = 0; s0 < S; s0 += kReduceTile) {
+    const unsigned T = min((unsigned)kReduceTile, S - s0);
+    // Runs of a tile: 32 doubles (256 B) of t and 32 uint16 (64 B) of k per
+    // pixel. With s_count % 4 == 0 they are 16-B aligned: t is read 16 lanes x
+    // 16 B per pixel, 4 pixels per load, k 8 lanes x 8 B, 8 pixels per load;
+    // else element by element. Every load is in flight before the first LDS
+    // store.
+    static_assert(kReduceTile == 32 && kReduceBlock == 64, "tile shape of the loads below");
+    const unsigned P = S;
+    if (S % 4 == 0) {
+    double2 vt[16];
+    uint2 vk[8];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const unsigned p = 4 * i + (lane >> 4), j = (lane & 15) * 2;
+      vt[i] = make_double2(0.0, 0.0);
+      if (q0 + p < a.pixels && j < T)
+        vt[i] = *(const double2*)(a.samp_t + (size_t)(q0 + p) * P + s0 + j);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const unsigned p = 8 * i + (lane >> 3), j = (lane & 7) * 4;
+      vk[i] = make_uint2(0u, 0u);
+      if (q0 + p < a.pixels && j < T)
+        vk[i] = *(const uint2*)(a.samp_k + (size_t)(q0 + p) * P + s0 + j);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      *(double2*)&s_t[4 * i + (lane >> 4)][(lane & 15) * 2] = vt[i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      *(uint2*)&s_k[8 * i + (lane >> 3)][(lane & 7) * 4] = vk[i];
+    } else {
+      double vt[8];
+      unsigned short vk[8];
+      for (int h = 0; h < 4; ++h) {
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const unsigned p = 16 * h + 2 * i + (lane >> 5), j = lane & 31;
+          const bool ok = q0 + p < a.pixels && j < T;
+          const size_t u = (size_t)(q0 + p) * S + s0 + j;
+          vt[i] = ok ? a.samp_t[u] : 0.0;
+          vk[i] = ok ? a.samp_k[u] : (unsigned short)0;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          s_t[16 * h + 2 * i + (lane >> 5)][lane & 31] = vt[i];
+          s_k[16 * h + 2 * i + (lane >> 5)][lane & 31] = vk[i];
+        }
+      }
+    }
+    __syncthreads();
+    for (unsigned j = 0; j < T; ++j) {
+      double cr, cg, cb;
+      sample_colour(s_t[lane][j], s_k[lane][j], cr, cg, cb);
+      r += cr;
+      g += cg;
+      b += cb;
+    }
   }
+  if (q >= a.pixels) return;
   if (a.accum) {
     a.accum[(size_t)q * 3 + 0] = r;
     a.accum[(size_t)q * 3 + 1] = g;

@@ -177,7 +177,7 @@ def test_multi_chunk_large_spp(oracle_mod, tmp_path):
     import sys
     sph = oracle_mod.scene_two_spheres()
     cam = oracle_mod.camera_default()
-    w, h, spp = 64, 36, 200  # 64*36*24 B = 55 KB per sample -> 19 samples per 1 MB chunk
+    w, h, spp = 64, 36, 200  # 64*36*10 B = 23 KB per sample -> 44-sample chunks of 1 MB
     want, _, _ = oracle_mod.render(sph, cam, w, h, spp, threads=8)
     code = ("import numpy as np, petershirleyraytracer_amd as P;"
             f"a,_,_=P.render(P.scene_two_spheres(),P.camera_default(),{w},{h},{spp});"
