@@ -83,6 +83,8 @@ def parse():
                          "(default: each rank quantises its rows, uint8 gather)")
     ap.add_argument("--no-fixpoint", action="store_true",
                     help="trace provably trapped paths to max_depth (DESIGN.md §9)")
+    ap.add_argument("--pipeline", type=int, default=2,
+                    help="frames in flight (1 = each frame waits for the previous one)")
     ap.add_argument("--emulate-shard", default="",
                     help="R/G: one process renders only rank R's rows of a G-GPU run "
                          "(per-rank step time of the multi-GPU bench, on one GPU; "
@@ -201,15 +203,30 @@ def main():
     from petershirleyraytracer_amd.dist import gather_frame, rows_owned, shard
     from petershirleyraytracer_amd.render import FLAG_NO_CULL, FLAG_NO_FIXPOINT
 
+    if os.environ.get("PSRT_BENCH_BACKEND", "nccl") != "nccl":
+        local = 0  # rehearsal: every rank on the one GPU
     torch.cuda.set_device(local)
     distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ or "MASTER_PORT" in os.environ
     if distributed:  # one process per GPU over RCCL (backend "nccl" on ROCm)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # PSRT_BENCH_BACKEND=gloo: rehearse N ranks on one GPU (RCCL refuses
+        # two ranks on one device); the product path is RCCL
+        backend = os.environ.get("PSRT_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     w, h, spp = cfg["width"], cfg["height"], cfg["spp"]
     spheres, cam = scene_of(cfg)
-    ctx = P.Context(local)
-    ctx.set_scene(spheres, cam)
+    # Frames in flight: each slot has its own context (work queue, sample
+    # buffer, stats), stream and output rows, so frame k+1 fills the CUs that
+    # frame k's last waves release (DESIGN.md §7 "Frame pipelining").
+    depth = max(1, args.pipeline)
+    ctxs = []
+    for _ in range(depth):
+        c = P.Context(local)
+        c.set_scene(spheres, cam)
+        ctxs.append(c)
     if args.emulate_shard:
         if world != 1:
             raise SystemExit("--emulate-shard runs in a single process")
@@ -224,50 +241,107 @@ def main():
                    (FLAG_NO_CULL if args.no_cull else 0)
                    | (FLAG_NO_FIXPOINT if args.no_fixpoint else 0))
     dev = torch.device("cuda", local)
-    acc = torch.zeros((rows, w, 3), dtype=torch.float64, device=dev)
-    rgb = torch.zeros((h, w, 3), dtype=torch.uint8, device=dev) if rank == 0 else None
-    rgb_rows = torch.zeros((rows, w, 3), dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    acc = [torch.zeros((rows, w, 3), dtype=torch.float64, device=dev) for _ in range(depth)]
+    rgb = torch.zeros((h, w, 3), dtype=torch.uint8, device=dev) if rank == 0 and world > 1 else None
+    rgb_rows = [torch.zeros((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(depth)]
+    # each frame slot renders on its context's own stream
+    streams = [torch.cuda.ExternalStream(c.stream(), device=dev) for c in ctxs]
+    # N > 1: every gather goes on one stream, in frame order on every rank
+    comm = torch.cuda.Stream(dev)
 
     def barrier():
         if distributed:
             dist.barrier()
 
-    kernel_ms, rays, executed, elapsed = [], [], [], 0.0
     frame = None
-    for step in range(args.warmup + args.steps):
-        if step == args.warmup:
-            barrier()
-            torch.cuda.synchronize(dev)
-            t0 = time.perf_counter()
+    pending = [None] * depth  # per slot: (step, event after the frame's gather)
+    run = {"dn": depth, "warm": args.warmup, "kms": [], "rays": [], "exec": []}
+
+    def launch(step):
+        nonlocal frame
+        sl = step % run["dn"]
+        ctx, st = ctxs[sl], streams[sl]
         if world == 1:
-            ctx.render_device(prm, acc.data_ptr(), rgb.data_ptr(), stream.cuda_stream)
-            frame = gather_frame(acc, h, rank, world) if distributed else acc
-        elif args.gather_fp64:
-            ctx.render_device(prm, acc.data_ptr(), 0, stream.cuda_stream)
-            frame = gather_frame(acc, h, rank, world)
-            if rank == 0:
-                ctx.quantize_device(frame.data_ptr(), w, h, spp, rgb.data_ptr(),
-                                    stream.cuda_stream)
+            ctx.render_device(prm, acc[sl].data_ptr(), rgb_rows[sl].data_ptr(), st.cuda_stream)
+            frame = acc[sl]
+            pending[sl] = (step, None)
+            return
+        if args.gather_fp64:
+            ctx.render_device(prm, acc[sl].data_ptr(), 0, st.cuda_stream)
+            src = acc[sl]
         else:
             # write_color is per pixel: each rank quantises its own rows, and
             # the gather moves 3 B per pixel instead of 24 (C3: 2.9 MB, not 23)
-            ctx.render_device(prm, acc.data_ptr(), rgb_rows.data_ptr(), stream.cuda_stream)
-            frame = gather_frame(rgb_rows, h, rank, world)
+            ctx.render_device(prm, acc[sl].data_ptr(), rgb_rows[sl].data_ptr(), st.cuda_stream)
+            src = rgb_rows[sl]
+        comm.wait_stream(st)
+        with torch.cuda.stream(comm):
+            frame = gather_frame(src, h, rank, world)
             if rank == 0:
-                rgb.copy_(frame)
-        st = ctx.sync_stats()
-        if step >= args.warmup:
-            kernel_ms.append(st["kernel_ms"])
-            rays.append(st["rays"])
-            executed.append((st["tests_executed"], st["box_tests"], st["rays_traced"]))
-    torch.cuda.synchronize(dev)
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+                if args.gather_fp64:
+                    ctxs[sl].quantize_device(frame.data_ptr(), w, h, spp, rgb.data_ptr(),
+                                             comm.cuda_stream)
+                else:
+                    rgb.copy_(frame)
+            ev = torch.cuda.Event()
+            ev.record(comm)
+        pending[sl] = (step, ev)
+
+    def retire(sl):
+        """Wait for the slot's frame (render + gather) and collect its stats."""
+        if pending[sl] is None:
+            return
+        step, ev = pending[sl]
+        st = ctxs[sl].sync_stats()
+        if ev is not None:
+            ev.synchronize()
+        pending[sl] = None
+        if step >= run["warm"]:
+            run["kms"].append(st["kernel_ms"])
+            run["rays"].append(st["rays"])
+            run["exec"].append((st["tests_executed"], st["box_tests"], st["rays_traced"]))
+
+    def drain():
+        for k in range(depth):
+            retire(k)
+        torch.cuda.synchronize(dev)
+
+    def timed(dn, nwarm, nsteps):
+        """nwarm untimed + nsteps timed frames, dn in flight; the timed frames
+        start from an idle GPU and end when the last one is done."""
+        run.update(dn=dn, warm=nwarm, kms=[], rays=[], exec=[])
+        for step in range(nwarm + nsteps):
+            if step == nwarm:
+                drain()
+                barrier()
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+            retire(step % dn)  # the slot's previous frame must be done
+            launch(step)
+        drain()
+        barrier()
+        el = time.perf_counter() - t0
+        if distributed:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    elapsed = timed(depth, args.warmup, args.steps)
+    last_slot = (args.warmup + args.steps - 1) % depth
+    if world == 1:
+        rgb = rgb_rows[last_slot]
+    # Kernel time for the roofline: frames one at a time (in flight together,
+    # a launch's HIP events also span the other frame's work).
+    unpiped = None
+    if depth > 1:
+        n1 = min(args.steps, 3)
+        el1 = timed(1, 0, n1)
+        unpiped = {"ms_per_step": round(el1 / n1 * 1e3, 3),
+                   "value": round((rows if args.emulate_shard else h) * w * spp * n1 / el1 / 1e6, 4)}
+    kernel_ms, rays, executed = run["kms"], run["rays"], run["exec"]
+    if world == 1:
+        frame = acc[last_slot]
 
     # an emulated shard processed only its own rows
     total_samples = (rows if args.emulate_shard else h) * w * spp * args.steps
@@ -345,7 +419,10 @@ def main():
                 # issue is the bound; frac above counts only the FP64 algorithm
                 "valu_issue": valu_issue,
             },
-            "rays_per_sample": round(float(np.sum(rays)) / (rows * w * spp * args.steps), 3),
+            "rays_per_sample": round(float(np.sum(rays)) / (rows * w * spp * len(rays)), 3),
+            "frames_in_flight": depth,
+            # the same frames rendered one at a time (each waits for the last)
+            "unpipelined": unpiped,
         }
         if args.save_ppm and rgb is not None:
             P.write_ppm(args.save_ppm, rgb.cpu().numpy(), binary=True)
@@ -359,7 +436,8 @@ def main():
         out["parity_vs_cpu"] = parity
         print(json.dumps(out), flush=True)
 
-    ctx.close()
+    for c in ctxs:
+        c.close()
     if distributed:
         dist.destroy_process_group()
 

@@ -137,6 +137,11 @@ int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres,
 int rt_render_device(rt_context* ctx, const rt_params* params, double* d_accum,
                      unsigned char* d_rgb8, void* stream);
 
+/* The context's own stream (hipStream_t as void*, non-blocking), used when
+ * rt_render_device gets stream == NULL. One context per frame in flight
+ * gives each frame its own stream (bench.py frame pipelining). */
+void* rt_context_stream(rt_context* ctx);
+
 /* Wait for the context's last render and fill stats (counters + kernel_ms). */
 int rt_context_sync_stats(rt_context* ctx, rt_stats* stats);
 

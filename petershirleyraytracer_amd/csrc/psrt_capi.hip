@@ -115,6 +115,7 @@ struct rt_context {
   std::vector<hipEvent_t> ev;  // pairs around each trace launch
   int ev_used = 0;
   hipEvent_t ev_all0 = nullptr, ev_all1 = nullptr;
+  hipStream_t last_stream = nullptr;  // stream of the last render (stats readback)
   rt_stats last{};
   int n_last = 0;
 };
@@ -577,6 +578,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipEventRecord(c->ev_all1, st));
+  c->last_stream = st;
   c->ev_used = nchunks;
   c->last = rt_stats{};
   c->last.samples = (uint64_t)P * p->spp;
@@ -584,12 +586,18 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   return RT_OK;
 }
 
+void* rt_context_stream(rt_context* c) { return c ? (void*)c->stream : nullptr; }
+
 int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   if (!c) return set_error(RT_E_INVALID, "rt_context_sync_stats: ctx is NULL");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipEventSynchronize(c->ev_all1));
   unsigned long long cnt[4] = {0, 0, 0, 0};
-  HIP_TRY(hipMemcpy(cnt, c->d_counters + 1, sizeof cnt, hipMemcpyDeviceToHost));
+  // on the render's own stream: a null-stream copy would also wait for work
+  // other contexts queued on other streams (a pipelined next frame)
+  HIP_TRY(hipMemcpyAsync(cnt, c->d_counters + 1, sizeof cnt, hipMemcpyDeviceToHost,
+                         c->last_stream));
+  HIP_TRY(hipStreamSynchronize(c->last_stream));
   const unsigned long long rays = cnt[0];
   double kms = 0.0;
   for (int ch = 0; ch < c->ev_used; ++ch) {

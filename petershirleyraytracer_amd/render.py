@@ -212,6 +212,10 @@ class Context:
         check(self._L.rt_render_device(self.handle, C.byref(p), d_accum or None,
                                        d_rgb8 or None, stream or None), "rt_render_device")
 
+    def stream(self) -> int:
+        """The context's own hipStream_t (as an int), used for stream=0."""
+        return self._L.rt_context_stream(self.handle) or 0
+
     def sync_stats(self) -> dict:
         st = RtStats()
         check(self._L.rt_context_sync_stats(self.handle, C.byref(st)), "rt_context_sync_stats")
