@@ -83,8 +83,9 @@ def parse():
                          "(default: each rank quantises its rows, uint8 gather)")
     ap.add_argument("--no-fixpoint", action="store_true",
                     help="trace provably trapped paths to max_depth (DESIGN.md §9)")
-    ap.add_argument("--pipeline", type=int, default=2,
-                    help="frames in flight (1 = each frame waits for the previous one)")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="frames in flight (1 = each frame waits for the previous one; "
+                         "0 = auto: 3 for per-rank frames of <= 32 M samples, else 2)")
     ap.add_argument("--emulate-shard", default="",
                     help="R/G: one process renders only rank R's rows of a G-GPU run "
                          "(per-rank step time of the multi-GPU bench, on one GPU; "
@@ -221,12 +222,6 @@ def main():
     # Frames in flight: each slot has its own context (work queue, sample
     # buffer, stats), stream and output rows, so frame k+1 fills the CUs that
     # frame k's last waves release (DESIGN.md §7 "Frame pipelining").
-    depth = max(1, args.pipeline)
-    ctxs = []
-    for _ in range(depth):
-        c = P.Context(local)
-        c.set_scene(spheres, cam)
-        ctxs.append(c)
     if args.emulate_shard:
         if world != 1:
             raise SystemExit("--emulate-shard runs in a single process")
@@ -240,6 +235,15 @@ def main():
     prm = P.params(w, h, spp, args.max_depth, args.seed, off, stride,
                    (FLAG_NO_CULL if args.no_cull else 0)
                    | (FLAG_NO_FIXPOINT if args.no_fixpoint else 0))
+    # auto: 3 in flight for short per-rank frames (<= 32 M samples: the tail
+    # is a large share), else 2 (a third frame then shares the GPU with the
+    # second for its whole run and the full C3 frame gets slower)
+    depth = args.pipeline if args.pipeline > 0 else (3 if rows * w * spp <= 32_000_000 else 2)
+    ctxs = []
+    for _ in range(depth):
+        c = P.Context(local)
+        c.set_scene(spheres, cam)
+        ctxs.append(c)
     dev = torch.device("cuda", local)
     acc = [torch.zeros((rows, w, 3), dtype=torch.float64, device=dev) for _ in range(depth)]
     rgb = torch.zeros((h, w, 3), dtype=torch.uint8, device=dev) if rank == 0 and world > 1 else None

@@ -12,6 +12,6 @@ for sh in ${SHARDS:-0/1 0/8}; do
     python3 -c "import json; d=json.loads(open('gpurun_out/pipe_$i.log').read().strip().splitlines()[-1]); print('$sh depth $d', d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'])"
   done
 done
-PSRT_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 4 --warmup 1 > gpurun_out/pipe_gloo2.log 2>&1
+PSRT_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${NPROC:-2} --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus ${NPROC:-2} --steps 4 --warmup 1 > gpurun_out/pipe_gloo2.log 2>&1
 rc=$?; echo "gloo2 rc=$rc"; tail -1 gpurun_out/pipe_gloo2.log | cut -c1-400
 exit $rc
