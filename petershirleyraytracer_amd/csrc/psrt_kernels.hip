@@ -35,6 +35,10 @@
 #define PSRT_SLAB_ASM 1  // slab test min/max as inline asm (no per-box NaN canonicalisation)
 #endif
 
+#ifndef PSRT_TAIL_PRIO
+#define PSRT_TAIL_PRIO 0  // s_setprio of a wave once the work queue is empty (0 = unchanged)
+#endif
+
 namespace psrt {
 
 __device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
@@ -891,6 +895,9 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       }
       if (win_base >= total) {
         exhausted = true;
+        // Launch tail: this wave's remaining paths decide when the launch
+        // (and the next frame's start on its CUs) ends; let them issue first.
+        if constexpr (PSRT_TAIL_PRIO > 0) __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
         if constexpr (kStamps) {
           const unsigned long long t = __builtin_amdgcn_s_memrealtime();
           if (wlog && lane == 0) wlog[1] = t, wlog[3] = iters;
