@@ -62,6 +62,8 @@ BOX_OPS_FP64_EQ = 7  # FP32 slab test: 6 FMA + 7 min/max + compare = 14 FP32 ops
 # scatter 26 (vec3.h:102-109, main.cc:42-43, the new ray's A), look-ahead
 # trials 9 x 1.91 per scatter (vec3.h:83-95) ~ 17  ->  ~61
 SHADE_OPS_PER_RAY = 61
+# one finished sample's record in HBM: t (FP64) + k (uint16) (psrt_kernels.h kSampleBytes)
+SAMPLE_RECORD_BYTES = 10
 
 
 def parse():
@@ -85,7 +87,8 @@ def parse():
                     help="trace provably trapped paths to max_depth (DESIGN.md §9)")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="frames in flight (1 = each frame waits for the previous one; "
-                         "0 = auto: 3 for per-rank frames of <= 32 M samples, else 2)")
+                         "0 = auto: 1 for multi-chunk frames, 3 for per-rank frames of "
+                         "<= 32 M samples, else 2)")
     ap.add_argument("--emulate-shard", default="",
                     help="R/G: one process renders only rank R's rows of a G-GPU run "
                          "(per-rank step time of the multi-GPU bench, on one GPU; "
@@ -235,10 +238,20 @@ def main():
     prm = P.params(w, h, spp, args.max_depth, args.seed, off, stride,
                    (FLAG_NO_CULL if args.no_cull else 0)
                    | (FLAG_NO_FIXPOINT if args.no_fixpoint else 0))
-    # auto: 3 in flight for short per-rank frames (<= 32 M samples: the tail
-    # is a large share), else 2 (a third frame then shares the GPU with the
-    # second for its whole run and the full C3 frame gets slower)
-    depth = args.pipeline if args.pipeline > 0 else (3 if rows * w * spp <= 32_000_000 else 2)
+    # auto: overlap only frame tails. Two persistent launches that share the
+    # GPU for their whole run are slower than one after the other (C4: -8%).
+    # So: 1 in flight when a frame takes several sample chunks (the next
+    # frame would share the GPU with every chunk after the first), 3 for
+    # short per-rank frames (<= 32 M samples: the tail is a large share),
+    # else 2 (a third frame then shares the GPU with the second throughout).
+    per_rank = rows * w * spp
+    buf_cap = int(os.environ.get("PSRT_SAMPLE_BUF_MB", "16384")) << 20  # psrt_capi.hip
+    if args.pipeline > 0:
+        depth = args.pipeline
+    elif per_rank * SAMPLE_RECORD_BYTES > buf_cap:
+        depth = 1
+    else:
+        depth = 3 if per_rank <= 32_000_000 else 2
     ctxs = []
     for _ in range(depth):
         c = P.Context(local)
@@ -371,7 +384,7 @@ def main():
         # algorithmic HBM bytes of one psrt_trace launch: each sample's record
         # (t: 8 B, k: 2 B) written once; the 485 x 40 B sphere list is L2-resident
         samples_rank = rows * w * spp
-        hbm_alg = samples_rank * 10
+        hbm_alg = samples_rank * SAMPLE_RECORD_BYTES
         traffic, valu_issue = profile_counters(args.config)
         out = {
             "metric": METRIC,

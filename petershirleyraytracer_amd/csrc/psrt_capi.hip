@@ -71,7 +71,8 @@ psrt::FastDiv fast_div_make(unsigned d) {
 
 size_t sample_buffer_cap_bytes() {
   const char* e = std::getenv("PSRT_SAMPLE_BUF_MB");
-  size_t mb = e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)4096;
+  // default 16 GiB: C4 (41 GB of sample records) in 3 chunks, C5 in 6
+  size_t mb = e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)16384;
   if (mb < 1) mb = 1;
   return mb << 20;
 }
