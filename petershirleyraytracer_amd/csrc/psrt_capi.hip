@@ -110,6 +110,11 @@ struct rt_context {
   size_t accum_tmp_cap = 0;  // doubles
   uint4* d_plist = nullptr;  // camera-ray candidate lists, one uint4 per owned pixel
   size_t plist_cap = 0;      // records
+  // The lists depend only on the scene, camera, frame size and shard: they
+  // are built once per (set_scene, W, H, row_offset, row_stride) and reused.
+  bool plist_valid = false;
+  int plist_key[4] = {0, 0, 0, 0};
+  hipEvent_t ev_plist = nullptr;  // after the lists' build (other streams wait on it)
   unsigned long long* d_wave_log = nullptr;  // diagnostic (PSRT_STAMPS): per-wave timeline
   size_t wave_log_cap = 0, wave_log_used = 0;
   unsigned long long* d_counters = nullptr;  // [0] queue head, [1] rays, [2] tests, [3] boxes
@@ -197,6 +202,7 @@ int rt_context_create(int device, rt_context** out) {
   HIP_TRY(hipMalloc(&c->d_counters, 64 * sizeof(unsigned long long)));
   HIP_TRY(hipEventCreate(&c->ev_all0));
   HIP_TRY(hipEventCreate(&c->ev_all1));
+  HIP_TRY(hipEventCreateWithFlags(&c->ev_plist, hipEventDisableTiming));
   *out = c;
   return RT_OK;
 }
@@ -223,6 +229,7 @@ int rt_context_destroy(rt_context* c) {
   for (auto e : c->ev) (void)hipEventDestroy(e);
   if (c->ev_all0) (void)hipEventDestroy(c->ev_all0);
   if (c->ev_all1) (void)hipEventDestroy(c->ev_all1);
+  if (c->ev_plist) (void)hipEventDestroy(c->ev_plist);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return RT_OK;
@@ -258,6 +265,7 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
   }
   c->n = n;
   c->cam = *cam;
+  c->plist_valid = false;
   // exact culling structure
   const psrt::BvhHost b = psrt::build_bvh(sph, n);
   (void)hipFree(c->d_nodes);
@@ -506,9 +514,14 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     c->plist_cap = 0;
     HIP_TRY(hipMalloc(&c->d_plist, P * sizeof(uint4)));
     c->plist_cap = P;
+    c->plist_valid = false;
   }
   HIP_TRY(hipEventRecord(c->ev_all0, st));
-  if (camlist) {
+  const int key[4] = {p->width, p->height, p->row_offset, p->row_stride};
+  if (camlist && c->plist_valid && std::equal(key, key + 4, c->plist_key)) {
+    HIP_TRY(hipStreamWaitEvent(st, c->ev_plist, 0));  // built on another stream, maybe
+    bv.plist = c->d_plist;
+  } else if (camlist) {
     psrt::CamListArgs la{};
     for (int k = 0; k < 3; ++k) {
       la.org[k] = c->cam.origin[k];
@@ -530,6 +543,9 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
                   (rows + psrt::kCamTile - 1) / psrt::kCamTile);
     hipLaunchKernelGGL(psrt::psrt_camera_lists, lg, dim3(64), 0, st, la);
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev_plist, st));
+    std::copy(key, key + 4, c->plist_key);
+    c->plist_valid = true;
     bv.plist = c->d_plist;
   }
   for (int ch = 0; ch < nchunks; ++ch) {

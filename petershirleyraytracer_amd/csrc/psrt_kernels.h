@@ -29,7 +29,7 @@ constexpr int kReduceBlock = 64;   // psrt_reduce: one wave per 64 pixels
 #ifndef PSRT_REDUCE_TILE
 #define PSRT_REDUCE_TILE 32
 #endif
-constexpr int kReduceTile = PSRT_REDUCE_TILE;  // (the loads assume 32)  // samples per pixel staged per LDS tile
+constexpr int kReduceTile = PSRT_REDUCE_TILE;  // samples per pixel per LDS tile: 16 or 32
 constexpr size_t kSampleBytes = sizeof(double) + sizeof(unsigned short);
 
 struct TraceArgs {

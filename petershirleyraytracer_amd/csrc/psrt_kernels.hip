@@ -1132,8 +1132,8 @@ PSRT_INSTANTIATE(true, true, true)
 // last chunk (color.h:8-24).
 __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
   // One wave per 64 pixels. A pixel's samples are contiguous, so the wave
-  // stages [64 pixels][32 samples] tiles through LDS with 256-B runs per
-  // pixel, then each lane adds its pixel's samples in order.
+  // stages [64 pixels][kReduceTile samples] tiles through LDS, then each lane
+  // adds its pixel's samples in order.
   __shared__ __attribute__((aligned(16))) double s_t[kReduceBlock][kReduceTile + 2];
   __shared__ __attribute__((aligned(16))) unsigned short s_k[kReduceBlock][kReduceTile + 4];
   const unsigned lane = threadIdx.x;
@@ -1148,45 +1148,48 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
   }
   for (unsigned s0 = 0; s0 < S; s0 += kReduceTile) {
     const unsigned T = min((unsigned)kReduceTile, S - s0);
-    // Runs of a tile: 32 doubles (256 B) of t and 32 uint16 (64 B) of k per
-    // pixel. With s_count % 4 == 0 they are 16-B aligned: t is read 16 lanes x
-    // 16 B per pixel, 4 pixels per load, k 8 lanes x 8 B, 8 pixels per load;
-    // else element by element. Every load is in flight before the first LDS
-    // store.
-    static_assert(kReduceTile == 32 && kReduceBlock == 64, "tile shape of the loads below");
-    const unsigned P = S;
+    // Runs of a tile: kReduceTile doubles of t and kReduceTile uint16 of k
+    // per pixel. With s_count % 4 == 0 they are 16-B aligned: t is read in
+    // 16-B pieces (kLT lanes per pixel), k in 8-B pieces (kLK lanes per
+    // pixel); else element by element. Every load of a pass is in flight
+    // before the first LDS store.
+    constexpr int kLT = kReduceTile / 2, kPT = 64 / kLT;  // t: lanes, pixels per load
+    constexpr int kLK = kReduceTile / 4, kPK = 64 / kLK;  // k: lanes, pixels per load
+    static_assert(kReduceBlock == 64 && (kReduceTile == 16 || kReduceTile == 32),
+                  "tile shape of the loads below");
     if (S % 4 == 0) {
-    double2 vt[16];
-    uint2 vk[8];
+      double2 vt[kLT];
+      uint2 vk[kLK];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const unsigned p = 4 * i + (lane >> 4), j = (lane & 15) * 2;
-      vt[i] = make_double2(0.0, 0.0);
-      if (q0 + p < a.pixels && j < T)
-        vt[i] = *(const double2*)(a.samp_t + (size_t)(q0 + p) * P + s0 + j);
-    }
+      for (int i = 0; i < kLT; ++i) {
+        const unsigned p = kPT * i + lane / kLT, j = (lane % kLT) * 2;
+        vt[i] = make_double2(0.0, 0.0);
+        if (q0 + p < a.pixels && j < T)
+          vt[i] = *(const double2*)(a.samp_t + (size_t)(q0 + p) * S + s0 + j);
+      }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const unsigned p = 8 * i + (lane >> 3), j = (lane & 7) * 4;
-      vk[i] = make_uint2(0u, 0u);
-      if (q0 + p < a.pixels && j < T)
-        vk[i] = *(const uint2*)(a.samp_k + (size_t)(q0 + p) * P + s0 + j);
-    }
-    __syncthreads();
+      for (int i = 0; i < kLK; ++i) {
+        const unsigned p = kPK * i + lane / kLK, j = (lane % kLK) * 4;
+        vk[i] = make_uint2(0u, 0u);
+        if (q0 + p < a.pixels && j < T)
+          vk[i] = *(const uint2*)(a.samp_k + (size_t)(q0 + p) * S + s0 + j);
+      }
+      __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      *(double2*)&s_t[4 * i + (lane >> 4)][(lane & 15) * 2] = vt[i];
+      for (int i = 0; i < kLT; ++i)
+        *(double2*)&s_t[kPT * i + lane / kLT][(lane % kLT) * 2] = vt[i];
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-      *(uint2*)&s_k[8 * i + (lane >> 3)][(lane & 7) * 4] = vk[i];
+      for (int i = 0; i < kLK; ++i)
+        *(uint2*)&s_k[kPK * i + lane / kLK][(lane % kLK) * 4] = vk[i];
     } else {
+      constexpr int kPP = 64 / kReduceTile;  // pixels per load
       double vt[8];
       unsigned short vk[8];
-      for (int h = 0; h < 4; ++h) {
+      for (int h = 0; h < kReduceTile / 8; ++h) {
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const unsigned p = 16 * h + 2 * i + (lane >> 5), j = lane & 31;
+          const unsigned p = 8 * kPP * h + kPP * i + lane / kReduceTile, j = lane % kReduceTile;
           const bool ok = q0 + p < a.pixels && j < T;
           const size_t u = (size_t)(q0 + p) * S + s0 + j;
           vt[i] = ok ? a.samp_t[u] : 0.0;
@@ -1194,8 +1197,8 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          s_t[16 * h + 2 * i + (lane >> 5)][lane & 31] = vt[i];
-          s_k[16 * h + 2 * i + (lane >> 5)][lane & 31] = vk[i];
+          s_t[8 * kPP * h + kPP * i + lane / kReduceTile][lane % kReduceTile] = vt[i];
+          s_k[8 * kPP * h + kPP * i + lane / kReduceTile][lane % kReduceTile] = vk[i];
         }
       }
     }
