@@ -384,7 +384,7 @@ static void queue_phases(psrt::TraceArgs& ta, int grid, bool guided) {
   const char* ek = std::getenv("PSRT_QUEUE_K");
   const char* ed = std::getenv("PSRT_QUEUE_D");
   const double k = ek ? std::atof(ek) : 1.0;
-  const double d = ed ? std::atof(ed) : 8.0;
+  const double d = ed ? std::atof(ed) : 4.0;  // 8 before frame pipelining (bench.py)
   const uint64_t waves = (uint64_t)grid * (psrt::kTraceBlock / 64);
   unsigned s0 = guided ? psrt::kWorkChunk : psrt::kLinearChunk;
   while (guided && s0 > 64 && (double)ta.total_units < d * (double)waves * (double)s0) s0 >>= 1;
