@@ -83,7 +83,7 @@ inline frame render(const hittable_list& world, const camera& cam, int width, in
   f.height = height;
   f.spp = spp;
   f.rows = rt_rows_owned(height, row_offset, row_stride);
-  if (f.rows <= 0) throw std::invalid_argument("psrt::render: shard owns no rows");
+  if (f.rows < 0) f.rows = 0;  // a shard that owns no rows renders nothing
   f.accum.resize((size_t)f.rows * width * 3);
   f.rgb8.resize((size_t)f.rows * width * 3);
   check(rt_render(spheres.data(), (int)spheres.size(), &c, &p, f.accum.data(), f.rgb8.data(),

@@ -20,6 +20,14 @@
  *   - Pixel order is the reference's output order (main.cc:72-75): output row
  *     r = 0 is the TOP row (reference j = H-1), columns i = 0..W-1 left to
  *     right. A shard owns rows r = row_offset + k*row_stride, k = 0,1,...
+ *   - Threads and streams. rt_render and the rt_debug_* entries may be
+ *     called from any number of host threads: they share the device's
+ *     default context and hold a per-device lock for the whole call. An
+ *     rt_context is used by one host thread at a time. Its renders may go to
+ *     different streams: they share the context's device buffers, so the
+ *     library orders them (a render on a new stream waits for the previous
+ *     render on the device; rt_context_set_scene and buffer growth wait for it
+ *     on the host). Frames meant to overlap use one context each.
  *   - Arithmetic is IEEE binary64 in the reference's operation order, no FMA
  *     contraction: accumulators are bit-identical to the reference's
  *     pixel_color (main.cc:77-84) for the same RNG stream.
@@ -130,7 +138,9 @@ int rt_context_destroy(rt_context* ctx);
 int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres,
                          int n_spheres, const rt_camera* cam);
 
-/* Enqueue a render of the owned rows on `stream`. d_accum (device,
+/* Enqueue a render of the owned rows on `stream` (after the context's
+ * previous render, whatever its stream). A shard that owns no rows
+ * (row_offset >= height) enqueues nothing and reports zero counters. d_accum (device,
  * rows_owned*width*3 doubles) and d_rgb8 (device, rows_owned*width*3 bytes)
  * may each be NULL. Returns after enqueueing; synchronise the stream before
  * reading. rt_context_sync_stats() reports the finished call's counters. */

@@ -122,6 +122,11 @@ struct rt_context {
   int ev_used = 0;
   hipEvent_t ev_all0 = nullptr, ev_all1 = nullptr;
   hipStream_t last_stream = nullptr;  // stream of the last render (stats readback)
+  // A render was enqueued and ev_all1 marks its end. The device buffers above
+  // are shared by every render of the context, whatever its stream: a render
+  // on another stream waits for ev_all1 on the device, and host-side writes
+  // (set_scene, reallocation) wait for it on the host (quiesce).
+  bool in_flight = false;
   rt_stats last{};
   int n_last = 0;
 };
@@ -137,8 +142,18 @@ int ensure_events(rt_context* c, int pairs) {
   return RT_OK;
 }
 
-int ensure_buf(double** p, size_t* cap, size_t need) {
+// Host wait for the context's last enqueued render (any stream): before the
+// host writes or frees a buffer that render may still read.
+int quiesce(rt_context* c) {
+  if (c->stream) HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->in_flight) HIP_TRY(hipEventSynchronize(c->ev_all1));
+  return RT_OK;
+}
+
+int ensure_buf(rt_context* c, double** p, size_t* cap, size_t need) {
   if (*cap >= need && *p) return RT_OK;
+  const int rc = quiesce(c);
+  if (rc) return rc;
   if (*p) (void)hipFree(*p);
   *p = nullptr;
   *cap = 0;
@@ -149,6 +164,9 @@ int ensure_buf(double** p, size_t* cap, size_t need) {
 
 std::mutex g_default_mu;
 rt_context* g_default[64] = {};
+// One-shot entries (rt_render, rt_debug_*) share their device's default
+// context: each holds that device's lock for the whole call.
+std::mutex g_device_mu[64];
 
 int default_device() {
   const char* e = std::getenv("RT_DEVICE");
@@ -239,7 +257,10 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
   if (!c || !cam || n < 0 || (n > 0 && !sph))
     return set_error(RT_E_INVALID, "rt_context_set_scene: bad arguments");
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  {  // the last render may run on any stream and still read geo / plist / BVH
+    const int rc = quiesce(c);
+    if (rc) return rc;
+  }
   const int cap = n > 0 ? n : 1;
   if (cap > c->n_cap) {
     (void)hipFree(c->d_geo);
@@ -358,7 +379,9 @@ static int check_params(const rt_params* p) {
   if (p->spp < 1) return set_error(RT_E_INVALID, "spp must be >= 1 (got %d)", p->spp);
   if (p->max_depth < -1 || p->max_depth > 100000)
     return set_error(RT_E_INVALID, "max_depth out of range (got %d)", p->max_depth);
-  if (p->row_stride < 1 || p->row_offset < 0 || p->row_offset >= p->height)
+  // row_offset >= height is a shard that owns no rows (more ranks than rows):
+  // its render is empty
+  if (p->row_stride < 1 || p->row_offset < 0)
     return set_error(RT_E_INVALID, "bad shard: row_offset %d row_stride %d height %d", p->row_offset,
                 p->row_stride, p->height);
   if ((long long)p->width * p->height >= (1LL << 32))
@@ -422,6 +445,21 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   hipStream_t st = stream_ ? (hipStream_t)stream_ : c->stream;
   const int rows = rt_rows_owned(p->height, p->row_offset, p->row_stride);
   const size_t P = (size_t)rows * p->width;
+  // The context's buffers (samples, counters, camera lists, events) are
+  // shared by its renders: a render on another stream than the last one
+  // starts after it (same stream: stream order already does it).
+  if (c->in_flight && st != c->last_stream) HIP_TRY(hipStreamWaitEvent(st, c->ev_all1, 0));
+  if (P == 0) {  // a shard that owns no rows: zero counters, no launch
+    HIP_TRY(hipMemsetAsync(c->d_counters + 1, 0, 63 * sizeof(unsigned long long), st));
+    HIP_TRY(hipEventRecord(c->ev_all0, st));
+    HIP_TRY(hipEventRecord(c->ev_all1, st));
+    c->in_flight = true;
+    c->last_stream = st;
+    c->ev_used = 0;
+    c->last = rt_stats{};
+    c->n_last = c->n;
+    return RT_OK;
+  }
 
   // sample chunking: the samples buffer holds s_chunk x P records of
   // kSampleBytes (t array, then k array), units < 2^32
@@ -436,11 +474,11 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   const int nchunks = (int)((p->spp + s_chunk - 1) / s_chunk);
   // t array (doubles) then k array (uint16), P x s_chunk records each
   const size_t recs = P * s_chunk;
-  rc = ensure_buf(&c->d_samples, &c->samples_cap, recs + (recs + 3) / 4);
+  rc = ensure_buf(c, &c->d_samples, &c->samples_cap, recs + (recs + 3) / 4);
   if (rc) return rc;
   double* acc = d_accum;
   if (!acc && nchunks > 1) {
-    rc = ensure_buf(&c->d_accum_tmp, &c->accum_tmp_cap, P * 3);
+    rc = ensure_buf(c, &c->d_accum_tmp, &c->accum_tmp_cap, P * 3);
     if (rc) return rc;
     acc = c->d_accum_tmp;
   }
@@ -473,6 +511,8 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   if (stamps) {
     const size_t need = (size_t)std::max(c->grid, c->grid_bvh) * (psrt::kTraceBlock / 64) * 5;
     if (c->wave_log_cap < need) {
+      rc = quiesce(c);
+      if (rc) return rc;
       (void)hipFree(c->d_wave_log);
       c->d_wave_log = nullptr;
       c->wave_log_cap = 0;
@@ -498,6 +538,20 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     if (ta.refill_min < 1) ta.refill_min = 1;
     const char* wt = std::getenv("PSRT_WALK_TAIL");  // tuning knob (default 4 lanes)
     ta.walk_tail = wt ? (unsigned)std::atoi(wt) : 4u;
+    // The kernel's per-lane counters are 32-bit; a lane flushes them in its
+    // wave's refill block once one reaches flush_at, and between two such
+    // blocks it adds at most one sample's work: <= max_depth + 1 rays (so
+    // `rays` is always exact), <= (max_depth + 1)(4n + 16) sphere / box tests
+    // (hint + big + list <= 2n + 16, leaves <= n; box tests <= 2 per node).
+    // flush_at leaves that much headroom below 2^32 (the test counts stay exact
+    // while one sample's tests are < 2^32). PSRT_FLUSH_AT: test knob, >= 1.
+    const uint64_t per_sample = (uint64_t)(p->max_depth + 1) * (4ull * (uint64_t)c->n + 16ull);
+    const uint64_t room = per_sample < 0xFFFFFFFFull ? 0xFFFFFFFFull - per_sample : 1ull;
+    ta.flush_at = (unsigned)std::max<uint64_t>(1ull, std::min<uint64_t>(room, 0x80000000ull));
+    if (const char* fa = std::getenv("PSRT_FLUSH_AT")) {
+      const unsigned long v = std::strtoul(fa, nullptr, 10);
+      if (v >= 1 && v < ta.flush_at) ta.flush_at = (unsigned)v;
+    }
   }
   const bool use_bvh = c->bvh && !(p->flags & RT_FLAG_NO_CULL);
   psrt::BvhView bv = bvh_view(c);
@@ -509,6 +563,8 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   const bool camlist = use_bvh && c->n < (int)psrt::kCamOverflow && om <= c->r_check &&
                        !std::getenv("PSRT_NO_CAMLIST");
   if (camlist && c->plist_cap < P) {
+    rc = quiesce(c);
+    if (rc) return rc;
     (void)hipFree(c->d_plist);
     c->d_plist = nullptr;
     c->plist_cap = 0;
@@ -595,6 +651,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipEventRecord(c->ev_all1, st));
+  c->in_flight = true;
   c->last_stream = st;
   c->ev_used = nchunks;
   c->last = rt_stats{};
@@ -607,6 +664,7 @@ void* rt_context_stream(rt_context* c) { return c ? (void*)c->stream : nullptr; 
 
 int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   if (!c) return set_error(RT_E_INVALID, "rt_context_sync_stats: ctx is NULL");
+  if (!c->in_flight) return set_error(RT_E_INVALID, "rt_context_sync_stats: no render enqueued");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipEventSynchronize(c->ev_all1));
   unsigned long long cnt[4] = {0, 0, 0, 0};
@@ -718,10 +776,14 @@ int rt_quantize_device(rt_context* c, const double* d_accum, int width, int rows
   return RT_OK;
 }
 
-static int get_default_context(rt_context** out) {
-  std::lock_guard<std::mutex> lk(g_default_mu);
-  int dev = default_device();
+// The default context of RT_DEVICE, returned with that device's lock held
+// in *lock: the one-shot entries run whole under it, so host threads calling
+// them on one device take turns instead of sharing buffers mid-call.
+static int get_default_context(rt_context** out, std::unique_lock<std::mutex>* lock) {
+  const int dev = default_device();
   if (dev < 0 || dev >= 64) return set_error(RT_E_INVALID, "RT_DEVICE out of range");
+  *lock = std::unique_lock<std::mutex>(g_device_mu[dev]);
+  std::lock_guard<std::mutex> lk(g_default_mu);
   if (!g_default[dev]) {
     int rc = rt_context_create(dev, &g_default[dev]);
     if (rc) return rc;
@@ -732,18 +794,22 @@ static int get_default_context(rt_context** out) {
 
 int rt_render(const rt_sphere* sph, int n, const rt_camera* cam, const rt_params* p,
               double* accum_rgb, unsigned char* rgb8, rt_stats* stats) {
-  if (!cam || !p || (!accum_rgb && !rgb8) || n < 0 || (n > 0 && !sph))
+  if (!cam || !p || n < 0 || (n > 0 && !sph))
     return set_error(RT_E_INVALID, "rt_render: bad arguments");
   int rc = check_params(p);
   if (rc) return rc;
+  // an empty shard (row_offset >= height) may pass no output buffers
+  if (!accum_rgb && !rgb8 && rt_rows_owned(p->height, p->row_offset, p->row_stride) > 0)
+    return set_error(RT_E_INVALID, "rt_render: no output buffer");
   rt_context* c = nullptr;
-  rc = get_default_context(&c);
+  std::unique_lock<std::mutex> lk;
+  rc = get_default_context(&c, &lk);
   if (rc) return rc;
   rc = rt_context_set_scene(c, sph, n, cam);
   if (rc) return rc;
   const int rows = rt_rows_owned(p->height, p->row_offset, p->row_stride);
   const size_t P = (size_t)rows * p->width;
-  rc = ensure_buf(&c->d_accum_tmp, &c->accum_tmp_cap, P * 3 + (P * 3 + 7) / 8);
+  rc = ensure_buf(c, &c->d_accum_tmp, &c->accum_tmp_cap, P * 3 + (P * 3 + 7) / 8 + 1);
   if (rc) return rc;
   double* d_acc = c->d_accum_tmp;
   unsigned char* d_rgb = (unsigned char*)(c->d_accum_tmp + P * 3);
@@ -751,9 +817,9 @@ int rt_render(const rt_sphere* sph, int n, const rt_camera* cam, const rt_params
   if (rc) return rc;
   rc = rt_context_sync_stats(c, stats);
   if (rc) return rc;
-  if (accum_rgb)
+  if (accum_rgb && P)
     HIP_TRY(hipMemcpy(accum_rgb, d_acc, P * 3 * sizeof(double), hipMemcpyDeviceToHost));
-  if (rgb8) HIP_TRY(hipMemcpy(rgb8, d_rgb, P * 3, hipMemcpyDeviceToHost));
+  if (rgb8 && P) HIP_TRY(hipMemcpy(rgb8, d_rgb, P * 3, hipMemcpyDeviceToHost));
   return RT_OK;
 }
 
@@ -762,7 +828,8 @@ int rt_debug_probe_f64(int op, const double* x, const double* y, double* out, in
   if (!x || !y || !out || n < 0) return set_error(RT_E_INVALID, "rt_debug_probe_f64: bad arguments");
   if (n == 0) return RT_OK;
   rt_context* c = nullptr;
-  int rc = get_default_context(&c);
+  std::unique_lock<std::mutex> lk;
+  int rc = get_default_context(&c, &lk);
   if (rc) return rc;
   double *dx, *dy, *dout;
   HIP_TRY(hipMalloc(&dx, n * sizeof(double)));
@@ -789,7 +856,8 @@ int rt_debug_world_hit(const rt_sphere* sph, int n, const double* rays, int coun
     return set_error(RT_E_INVALID, "rt_debug_world_hit: bad arguments");
   if (count == 0) return RT_OK;
   rt_context* c = nullptr;
-  int rc = get_default_context(&c);
+  std::unique_lock<std::mutex> lk;
+  int rc = get_default_context(&c, &lk);
   if (rc) return rc;
   rt_camera cam{};
   rc = rt_context_set_scene(c, sph, n, &cam);

@@ -60,6 +60,7 @@ struct TraceArgs {
   unsigned refill_min;              // idle lanes that trigger the finish + refill block
   unsigned walk_tail;               // a BVH pass stops once this few lanes still walk
   FastDiv div_s, div_w;             // unit / s_count, q / width
+  unsigned flush_at;                // per-lane counters flush to the totals at this value
 };
 
 struct BvhView {

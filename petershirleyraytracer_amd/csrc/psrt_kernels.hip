@@ -706,6 +706,23 @@ static_assert(PSRT_QDEPTH == 2 || PSRT_QDEPTH == 3, "queue slots q0..q2 exist");
                             // (6: 80 VGPRs, +2% over 5 despite 4 spilled VGPRs; 7 loses)
 #endif
 
+// rays / sphere tests / box tests of this wave (32-bit per lane) -> one 64-bit
+// atomic each. Called converged (whole wave).
+__device__ __forceinline__ void flush_counters(const TraceArgs& a, unsigned rays, unsigned spheres,
+                                            unsigned boxes, unsigned lane) {
+  unsigned long long wr = rays, ws = spheres, wb = boxes;
+  for (int off = 32; off > 0; off >>= 1) {
+    wr += __shfl_xor(wr, off);
+    ws += __shfl_xor(ws, off);
+    wb += __shfl_xor(wb, off);
+  }
+  if (lane == 0) {
+    if (wr) atomicAdd(a.ray_counter, wr);
+    if (ws) atomicAdd(a.ray_counter + 1, ws);
+    if (wb) atomicAdd(a.ray_counter + 2, wb);
+  }
+}
+
 template <bool kBVH, bool kStamps, bool kLds>
 __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(const double4* __restrict__ geo,
                                                           const double* __restrict__ inv_r,
@@ -729,6 +746,8 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   // the loop they would take ~40 registers and spill to scratch.
   __shared__ RefillConst s_rc;
   __shared__ GridC s_gc;
+  __shared__ unsigned long long s_flush[3];  // counters flushed from the lanes (refill block)
+  if (threadIdx.x < 3) s_flush[threadIdx.x] = 0ull;
   if (threadIdx.x == 0) s_gc = grid_consts(bv);
   if (threadIdx.x < 12)
     s_rc.cam[threadIdx.x] = threadIdx.x < 3   ? a.org[threadIdx.x]
@@ -816,6 +835,16 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     const bool run_block = need_mask != 0 && ((unsigned)__popcll(need_mask) >= a.refill_min ||
                                               need_mask == __ballot(1));
     if (run_block) {
+      // The per-lane counters are 32-bit. Between two runs of this block a lane
+      // adds at most one sample's work (it idles once its sample ends), which the
+      // host bounds below 2^32 - a.flush_at: flush them to the 64-bit totals
+      // once any lane's reaches a.flush_at (tests set it low to run this path).
+      if (__builtin_expect(__ballot(max(rays, max(cs.spheres, cs.boxes)) >= a.flush_at) != 0, 0)) {
+        atomicAdd(&s_flush[0], (unsigned long long)rays);  // LDS; to HBM at exit
+        atomicAdd(&s_flush[1], (unsigned long long)cs.spheres);
+        atomicAdd(&s_flush[2], (unsigned long long)cs.boxes);
+        rays = cs.spheres = cs.boxes = 0u;
+      }
       // sky (main.cc:46-48) x 0.5^k, or black; store
       if (done) {
         // The colour is a function of (t, k) alone (sample_colour): store those
@@ -1101,19 +1130,10 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   }
 
   if (PSRT_ABLATE && ablate_sink == 0x9E3779B9u && a.width < 0) samples[0] = ablate_sink;
-  // rays / sphere tests / box tests of this wave -> one atomic each
-  unsigned long long wr = rays, ws = cs.spheres, wb = cs.boxes;
-  for (int off = 32; off > 0; off >>= 1) {
-    wr += __shfl_xor(wr, off);
-    ws += __shfl_xor(ws, off);
-    wb += __shfl_xor(wb, off);
-  }
-  if (lane == 0) {
-    if (wr) atomicAdd(a.ray_counter, wr);
-    if (ws) atomicAdd(a.ray_counter + 1, ws);
-    if (wb) atomicAdd(a.ray_counter + 2, wb);
-    if (traced) atomicAdd(a.ray_counter + 3, traced);
-  }
+  flush_counters(a, rays, cs.spheres, cs.boxes, lane);
+  if (lane == 0 && traced) atomicAdd(a.ray_counter + 3, traced);
+  __syncthreads();  // every wave of the block has left the loop (and flushed to LDS)
+  if (threadIdx.x < 3 && s_flush[threadIdx.x]) atomicAdd(a.ray_counter + threadIdx.x, s_flush[threadIdx.x]);
 }
 
 #define PSRT_INSTANTIATE(B, S, L)                                                          \

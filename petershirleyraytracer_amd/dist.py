@@ -32,16 +32,24 @@ def rows_owned(height: int, rank: int, world: int) -> int:
 def gather_frame(local: torch.Tensor, height: int, rank: int, world: int,
                  dst: int = 0) -> Optional[torch.Tensor]:
     """Gather per-rank row blocks [rows_owned, W, C] into the full frame
-    [height, W, C] on rank `dst` (None elsewhere). One all_gather of blocks
-    padded to ceil(height/world) rows; de-interleave on the destination."""
+    [height, W, C] on rank `dst` (None elsewhere).
+
+    One gather to `dst` of blocks padded to ceil(height/world) rows: only the
+    destination receives them (an all_gather would send every block to every
+    rank). A rank that owns no rows (world > height) sends an all-padding
+    block. The destination then de-interleaves."""
     if world == 1:
         return local
     max_rows = rows_owned(height, 0, world)
+    mine = rows_owned(height, rank, world)
+    if local.shape[0] != mine:
+        raise ValueError(f"rank {rank} holds {local.shape[0]} rows, owns {mine}")
     w, ch = local.shape[1], local.shape[2]
     padded = local.new_zeros((max_rows, w, ch))
-    padded[: local.shape[0]] = local
-    parts = [torch.empty_like(padded) for _ in range(world)]
-    dist.all_gather(parts, padded)
+    if mine:
+        padded[:mine] = local
+    parts = [torch.empty_like(padded) for _ in range(world)] if rank == dst else None
+    dist.gather(padded, parts, dst=dst)
     if rank != dst:
         return None
     frame = local.new_empty((height, w, ch))

@@ -165,10 +165,9 @@ def render(spheres, camera, width: int, height: int, spp: int, max_depth: int = 
     cam = _camera(camera)
     p = params(width, height, spp, max_depth, seed, row_offset, row_stride,
                (0 if cull else FLAG_NO_CULL) | (0 if fixpoint else FLAG_NO_FIXPOINT))
-    rows = L.rt_rows_owned(height, row_offset, row_stride)
-    if rows <= 0:
-        raise _lib.RtError(f"shard owns no rows: height={height} offset={row_offset} "
-                           f"stride={row_stride}")
+    # a shard that owns no rows (row_offset >= height: more ranks than rows)
+    # renders nothing and returns empty [0, W, 3] blocks
+    rows = max(0, L.rt_rows_owned(height, row_offset, row_stride))
     acc = np.zeros((rows, width, 3), dtype=np.float64)
     rgb = np.zeros((rows, width, 3), dtype=np.uint8) if want_rgb else None
     st = RtStats()

@@ -100,8 +100,16 @@ def test_bad_arguments_are_errors():
     assert b"width/height" in L.rt_last_error()
     p = P.params(4, 4, 0)
     assert L.rt_render(None, 0, C.byref(cam), C.byref(p), acc, None, None) == -1
-    p = P.params(4, 4, 1, row_offset=4)
+    p = P.params(4, 4, 1, row_offset=-1)
     assert L.rt_render(None, 0, C.byref(cam), C.byref(p), acc, None, None) == -1
+    p = P.params(4, 4, 1, row_stride=0)
+    assert L.rt_render(None, 0, C.byref(cam), C.byref(p), acc, None, None) == -1
+    # row_offset >= height: a shard that owns no rows (more ranks than rows)
+    # is valid and may pass no output buffers; it fails only for want of a device
+    p = P.params(4, 4, 1, row_offset=4)
+    assert L.rt_rows_owned(4, 4, 1) == 0
+    assert L.rt_render(None, 0, C.byref(cam), C.byref(p), None, None, None) in (
+        (0,) if have_gpu() else (-2, -3))
     assert L.rt_render(None, 0, None, C.byref(p), acc, None, None) == -1
 
 

@@ -34,7 +34,10 @@ def _worker(rank, world, port, w, h, spp, out_path):
     off, stride = shard(rank, world)
     sph = O.scene_random_spheres(1)
     cam = O.camera_look_at(aspect=w / h)
-    acc, rgb, _ = O.render(sph, cam, w, h, spp, 50, 0, off, stride)
+    if rows_owned(h, rank, world):
+        acc, rgb, _ = O.render(sph, cam, w, h, spp, 50, 0, off, stride)
+    else:  # more ranks than rows: this rank sends an empty block
+        acc, rgb = np.zeros((0, w, 3)), np.zeros((0, w, 3), dtype=np.uint8)
     assert acc.shape[0] == rows_owned(h, rank, world)
     frame = gather_frame(torch.from_numpy(acc), h, rank, world)
     # bench.py's default N > 1 step: each rank quantises its rows (write_color
@@ -49,7 +52,7 @@ def _worker(rank, world, port, w, h, spp, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,h", [(2, 9), (3, 10), (2, 1)])
+@pytest.mark.parametrize("world,h", [(2, 9), (3, 10), (2, 1), (3, 2)])
 def test_gather_interleaved_rows(tmp_path, world, h):
     import oracle as O
     O.build()
