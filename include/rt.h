@@ -209,7 +209,8 @@ int rt_device_count(void);
 const char* rt_build_info(void);
 
 /* Debug: run one binary64 primitive on the device, element-wise
- * (op 0 sqrt(x), 1 x/y, 2 x*y, 3 x+y, 4 x*y+x uncontracted, 5 ldexp(x,(int)y)).
+ * (op 0 sqrt(x), 1 x/y, 2 x*y, 3 x+y, 4 x*y+x uncontracted, 5 ldexp(x,(int)y),
+ * 6 sqrt(x) as the trace kernel computes it).
  * Used by the numerics parity tests. */
 int rt_debug_probe_f64(int op, const double* x, const double* y, double* out, int n);
 

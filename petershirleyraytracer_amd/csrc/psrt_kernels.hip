@@ -138,20 +138,56 @@ __device__ __forceinline__ void sample_colour(double tt, unsigned short kk, doub
   }
 }
 
+#ifndef PSRT_FAST_SQRT
+#define PSRT_FAST_SQRT 1  // sqrt without the denormal scaling / class fixup where not needed
+#endif
+
+// sqrt (sphere.cc:19) as the compiler's correctly rounded f64 expansion
+// (v_rsq_f64, then Goldschmidt/Newton steps), minus its range handling: for
+// x >= 2^-767 the expansion's scaling is the identity and its zero / +inf
+// fixup is not taken, so the steps below are exactly the ones it runs. Other
+// inputs (0, tiny, +inf, NaN) take __builtin_sqrt behind a wave-uniform branch.
+__device__ __forceinline__ double sqrt_f64(double x) {
+#if PSRT_FAST_SQRT
+  const double r = __builtin_amdgcn_rsq(x);
+  double g = x * r;
+  double h = r * 0.5;
+  const double e = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, e, g);
+  h = __builtin_fma(h, e, h);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  const bool slow = !(x >= 0x1p-767 && x <= 0x1.fffffffffffffp1023);
+  if (__builtin_expect(__ballot(slow) != 0, 0)) {
+    if (slow) g = __builtin_sqrt(x);
+  }
+  return g;
+#else
+  return __builtin_sqrt(x);
+#endif
+}
+
 // Root selection of sphere.cc:24-31 over [0, tmax], bit for bit, with one
 // division where the reference may take two: the near root t1 = n1/A
 // (n1 = -hb - sq) is certainly < 0, and not -0, when n1 < -A*2^-900 (also
 // when A*2^-900 underflows: then |n1/A| >= 2^-1074/A > 2^-952); the far root
 // then decides, as in the reference. If t1 > tmax the far root is rejected
 // too: -hb + sq >= -hb - sq after rounding and division by A > 0 is
-// monotone, so t2 >= t1. A second division runs only for t1 in (-2^-900, 0).
+// monotone, so t2 >= t1. A second division runs only for t1 in (-2^-900, 0),
+// behind a wave-uniform branch: left to itself the compiler if-converts it and
+// every test pays both divisions (~13 VALU instructions and a v_rcp_f64 each).
 // NaN roots pass, as in the reference. Returns whether the root t is taken.
 __device__ __forceinline__ bool root_select(double hb, double sq, double A, double tmax,
                                             double& t) {
   const double n1 = -hb - sq;
   const bool far = n1 < -(A * 0x1p-900);
   t = (far ? -hb + sq : n1) / A;
-  if (!far && t < 0.0) t = (-hb + sq) / A;
+  const bool again = !far && t < 0.0;
+  if (__builtin_expect(__ballot(again) != 0, 0)) {
+    if (again) t = (-hb + sq) / A;
+  }
   return !(t < 0.0 || t > tmax);
 }
 
@@ -187,7 +223,7 @@ __device__ __forceinline__ int sweep_linear(const double4* __restrict__ geo, int
     }
     const double disc = hb * hb - A * c;
     if (!(disc < 0.0)) {
-      const double sq = __builtin_sqrt(disc);
+      const double sq = sqrt_f64(disc);
       double t;
       bool ok = true;
       if constexpr (kFix) {  // the trace path: tmin == 0
@@ -271,7 +307,7 @@ __device__ __forceinline__ bool test_sphere(const double4 s, int idx, double ox,
   const double hb = (dx * ax + dy * ay) + dz * az;
   const double disc = hb * hb - A * c;
   if (disc < 0.0) return true;
-  const double sq = __builtin_sqrt(disc);
+  const double sq = sqrt_f64(disc);
   double t;
   if (!root_select(hb, sq, A, best_t, t)) return true;
   if (t < best_t || idx > best_i) {  // equal t: the later index wins
@@ -1411,6 +1447,8 @@ __global__ void psrt_probe_f64(int op, const double* __restrict__ x,
     case 2: r = x[e] * y[e]; break;
     case 3: r = x[e] + y[e]; break;
     case 4: r = x[e] * y[e] + x[e]; break;  // must NOT contract
+    case 6: r = sqrt_f64(x[e]); break;        // the trace kernel's sqrt (fast path + fallback)
+
     default: r = __builtin_ldexp(x[e], (int)y[e]); break;
   }
   out[e] = r;

@@ -30,6 +30,7 @@ __global__ void __launch_bounds__(512) bench(unsigned long long* cyc, double* si
   const double dy = 1.0000001;
   const float fy = 1.0000001f;
   const unsigned uy = 0x4C957F2Du;
+  unsigned long long msk = __ballot(threadIdx.x & 1), mskw = 0;
   unsigned long long t0;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
   for (int it = 0; it < ITERS; ++it) {
@@ -67,6 +68,25 @@ __global__ void __launch_bounds__(512) bench(unsigned long long* cyc, double* si
         if constexpr (kOp == 26) asm volatile("v_mad_u32_u24 %0, %0, %1, %1" : "+v"(u[c]) : "v"(uy));
         if constexpr (kOp == 27) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(u[c]) : "v"(uy) : "vcc");
         if constexpr (kOp == 28) asm volatile("v_cvt_f64_u32 %0, %1" : "=v"(d[c]) : "v"(u[c]));
+        if constexpr (kOp == 29) asm volatile("v_add_u32 %0, %0, %1" : "+v"(u[c]) : "v"(uy));
+        if constexpr (kOp == 30) asm volatile("v_mov_b32 %0, %1" : "=v"(u[c]) : "v"(u[(c + 1) % CHAINS]));
+        if constexpr (kOp == 31) asm volatile("v_cmp_gt_u32 vcc, %0, %1" ::"v"(u[c]), "v"(uy) : "vcc");
+        if constexpr (kOp == 32) asm volatile("v_min_f32 %0, %0, %1" : "+v"(f[c]) : "v"(fy));
+        if constexpr (kOp == 33) asm volatile("v_max3_f32 %0, %0, %1, %1" : "+v"(f[c]) : "v"(fy));
+        if constexpr (kOp == 34) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(w[c]) : "v"(w[0]));
+        if constexpr (kOp == 35) asm volatile("v_and_b32 %0, %0, %1" : "+v"(u[c]) : "v"(uy));
+        if constexpr (kOp == 36) asm volatile("v_add_co_u32 %0, vcc, %0, %1" : "+v"(u[c]) : "v"(uy) : "vcc");
+        if constexpr (kOp == 37) asm volatile("v_cvt_f32_u32 %0, %1" : "=v"(f[c]) : "v"(u[c]));
+        if constexpr (kOp == 38) asm volatile("v_lshrrev_b32 %0, 7, %0" : "+v"(u[c]));
+        if constexpr (kOp == 39) asm volatile("v_cmp_class_f64 vcc, %0, %1" ::"v"(d[c]), "v"(uy) : "vcc");
+        if constexpr (kOp == 40) asm volatile("v_div_scale_f64 %0, vcc, %0, %1, %0" : "+v"(d[c]) : "v"(dy) : "vcc");
+        if constexpr (kOp == 41) asm volatile("v_div_fmas_f64 %0, %0, %1, %0" : "+v"(d[c]) : "v"(dy) : "vcc");
+        if constexpr (kOp == 42) asm volatile("v_mov_b64 %0, %1" : "=v"(w[c]) : "v"(w[(c + 1) % CHAINS]));
+        if constexpr (kOp == 44) asm volatile("v_cndmask_b32 %0, %0, %1, %2" : "+v"(u[c]) : "v"(uy), "s"(msk));
+        if constexpr (kOp == 45) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(u[c]) : "v"(uy));
+        if constexpr (kOp == 46) u[c] = (u[c] > uy) ? u[c] + uy : u[c] ^ uy;  // compiler-made cmp + select
+        if constexpr (kOp == 47) asm volatile("v_cmp_gt_u32 %0, %1, %2" : "=s"(mskw) : "v"(u[c]), "v"(uy));
+        if constexpr (kOp == 43) asm volatile("v_cndmask_b32 %0, %0, %1, vcc\n\tv_cndmask_b32 %0, %0, %1, vcc" : "+v"(u[c]) : "v"(uy) : "vcc");
       }
     }
   }
@@ -74,6 +94,7 @@ __global__ void __launch_bounds__(512) bench(unsigned long long* cyc, double* si
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
   double acc = 0;
   for (int c = 0; c < CHAINS; ++c) acc += d[c] + f[c] + u[c] + (double)w[c];
+  acc += (double)mskw;
   sink[blockIdx.x * blockDim.x + threadIdx.x] = acc;
   if (threadIdx.x % 64 == 0) atomicMax(cyc, t1 - t0);
 }
@@ -85,14 +106,21 @@ static const char* kNames[] = {"v_add_f64",    "v_mul_f64",     "v_fma_f64",    
                                "v_cvt_f32_f64", "v_min_f64",    "v_lshl_add_u64",
                                "v_lshlrev_b64", "v_lshrrev_b64", "v_alignbit_b32", "v_lshl_add_u32",
                                "v_xad_u32",    "v_sqrt_f64",    "v_mul_u32_u24", "v_mad_u32_u24",
-                               "v_cndmask_b32", "v_cvt_f64_u32"};
+                               "v_cndmask_b32", "v_cvt_f64_u32", "v_add_u32", "v_mov_b32",
+                               "v_cmp_gt_u32", "v_min_f32", "v_max3_f32", "v_pk_add_f32",
+                               "v_and_b32", "v_add_co_u32", "v_cvt_f32_u32", "v_lshrrev_b32",
+                               "v_cmp_class_f64", "v_div_scale_f64", "v_div_fmas_f64",
+                               "v_mov_b64", "2x v_cndmask_b32", "v_cndmask_b32 s-mask",
+                               "v_cndmask_b32_e32 vcc", "C select (cmp+cndmask+add+xor)",
+                               "v_cmp_gt_u32 -> sgpr"};
 
 template <int kOp>
 void run(int cus, double* sink, unsigned long long* dcyc) {
   const double n = (double)ITERS * UNROLL * CHAINS;
   double res[2];
-  const int waves[2] = {1, 8};
-  for (int m = 0; m < 2; ++m) {
+  const int waves[3] = {1, 2, 8};
+  double res3[3];
+  for (int m = 0; m < 3; ++m) {
     // waves per SIMD x 4 SIMDs per CU; one 256-thread block = 1 wave per SIMD
     const int blocks = cus * waves[m];
     (void)hipMemset(dcyc, 0, sizeof *dcyc);
@@ -102,10 +130,12 @@ void run(int cus, double* sink, unsigned long long* dcyc) {
     (void)hipMemcpy(&c, dcyc, sizeof c, hipMemcpyDeviceToHost);
     // max over waves of its loop cycles; with w waves sharing a SIMD the SIMD
     // issued w * n instructions in that time
-    res[m] = (double)c / (n * waves[m]);
+    res3[m] = (double)c / (n * waves[m]);
   }
-  std::printf("{\"insn\": \"%s\", \"cyc_per_wave_insn_1w\": %.3f, \"cyc_per_simd_insn_8w\": %.3f}\n",
-              kNames[kOp], res[0], res[1]);
+  (void)res;
+  std::printf("{\"insn\": \"%s\", \"cyc_per_wave_insn_1w\": %.3f, \"cyc_per_simd_insn_2w\": %.3f, "
+              "\"cyc_per_simd_insn_8w\": %.3f}\n",
+              kNames[kOp], res3[0], res3[1], res3[2]);
 }
 
 template <int... kOps>
@@ -127,7 +157,7 @@ int main() {
       hipMalloc(&dcyc, sizeof(unsigned long long)) != hipSuccess)
     return 1;
   run<0>(cus, sink, dcyc);  // warm-up (clocks)
-  run_all<0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28>(cus, sink, dcyc);
+  run_all<0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39, 40, 41, 42, 43, 44, 45, 46, 47>(cus, sink, dcyc);
   (void)hipFree(sink);
   (void)hipFree(dcyc);
   return 0;

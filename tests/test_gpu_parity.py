@@ -46,6 +46,23 @@ def test_sqrt_is_correctly_rounded():
     assert _same(P.probe_f64(0, x), np.sqrt(x))
 
 
+def test_kernel_sqrt_is_correctly_rounded():
+    """sqrt_f64: the expansion's steps without its range handling, plus the
+    full expansion behind a branch for 0, tiny, inf and NaN inputs."""
+    x, _ = _f64_inputs(seed=2)
+    rng = np.random.default_rng(8)
+    edge = np.array([2.0**-767, np.nextafter(2.0**-767, 0), np.nextafter(2.0**-767, 1), 2.0**-1022,
+                     5e-324, 1.7976931348623157e308, np.inf, -0.0, 0.0, -1.0, np.nan, 1e-300])
+    x = np.concatenate([x, edge, np.abs(rng.normal(size=200000)) * 10.0 ** rng.integers(-320, 308, 200000)])
+    got = P.probe_f64(6, x)
+    with np.errstate(invalid="ignore"):
+        assert _same(got, np.sqrt(x))
+    # the same lanes mixed in one wave: fast and slow lanes side by side
+    mix = np.where(np.arange(len(x)) % 3 == 0, 0.0, x)
+    with np.errstate(invalid="ignore"):
+        assert _same(P.probe_f64(6, mix), np.sqrt(mix))
+
+
 def test_division_is_correctly_rounded():
     x, y = _f64_inputs(seed=1)
     assert _same(P.probe_f64(1, x, y), x / y)
