@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 /* ---- error codes ---------------------------------------------------------- */
 #define RT_OK 0
@@ -221,6 +221,13 @@ int rt_debug_probe_f64(int op, const double* x, const double* y, double* out, in
  * go through the BVH path when the scene has one. */
 int rt_debug_world_hit(const rt_sphere* spheres, int n_spheres, const double* rays,
                        int count, double* out, int cull);
+
+/* Debug: as rt_debug_world_hit, with hints[k] (NULL = none; -1 = none for ray
+ * k) naming the sphere ray k starts on. The trace kernel tests a bounce ray's
+ * previous hit first and, from it, picks the neighbour list or direction map
+ * (DESIGN.md §11, §12); the record is the reference's whatever the hint. */
+int rt_debug_world_hit_hint(const rt_sphere* spheres, int n_spheres, const double* rays,
+                            const int* hints, int count, double* out, int cull);
 
 #ifdef __cplusplus
 }

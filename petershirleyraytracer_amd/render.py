@@ -271,15 +271,27 @@ def probe_f64(op: int, x: np.ndarray, y: Optional[np.ndarray] = None) -> np.ndar
     return out
 
 
-def world_hit(spheres, rays: np.ndarray, cull: bool = True) -> np.ndarray:
+def world_hit(spheres, rays: np.ndarray, cull: bool = True,
+              hints: Optional[np.ndarray] = None) -> np.ndarray:
     """hittable_list::hit on the device for rays[k] = (o, d, tmin, tmax);
     returns out[k] = (index, p, normal, t, front_face) (debug / KAT entry).
-    With cull, rays with tmin == 0, tmax == inf go through the BVH path."""
+    With cull, rays with tmin == 0, tmax == inf go through the BVH path;
+    hints[k] (optional, -1 = none) is the sphere ray k starts on, tested first
+    as the trace kernel tests a bounce ray's previous hit."""
     sp, n = _spheres(spheres)
     r = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 8)
     out = np.zeros((len(r), 9), dtype=np.float64)
     P = C.POINTER(C.c_double)
-    check(_lib.load().rt_debug_world_hit(sp, n, r.ctypes.data_as(P), len(r),
-                                         out.ctypes.data_as(P), 1 if cull else 0),
-          "rt_debug_world_hit")
+    if hints is None:
+        check(_lib.load().rt_debug_world_hit(sp, n, r.ctypes.data_as(P), len(r),
+                                             out.ctypes.data_as(P), 1 if cull else 0),
+              "rt_debug_world_hit")
+        return out
+    h = np.ascontiguousarray(hints, dtype=np.int32).reshape(-1)
+    if len(h) != len(r):
+        raise ValueError("hints: one per ray")
+    check(_lib.load().rt_debug_world_hit_hint(sp, n, r.ctypes.data_as(P),
+                                              h.ctypes.data_as(C.POINTER(C.c_int)), len(r),
+                                              out.ctypes.data_as(P), 1 if cull else 0),
+          "rt_debug_world_hit_hint")
     return out

@@ -100,6 +100,91 @@ def test_bvh_ties_and_degenerate_scenes():
         _compare(sph, o, rng.normal(size=(n, 3)))
 
 
+def _compare_hinted(sph, o, d, hint):
+    """The trace kernel's bounce-ray call (previous hit as the hint: the
+    neighbour-list and direction-map paths) against the reference scan."""
+    rays = np.concatenate([o, d, np.zeros((len(o), 1)), np.full((len(o), 1), np.inf)], 1)
+    a = world_hit(sph, rays, cull=True, hints=hint)
+    b = world_hit(sph, rays, cull=False)
+    same = (bits(a) == bits(b)) | (np.isnan(a) & np.isnan(b))
+    bad = np.where(~same.all(1))[0]
+    assert len(bad) == 0, (len(bad), rays[bad[:3]], hint[bad[:3]], a[bad[:3]], b[bad[:3]])
+    return (a[:, 0] >= 0).mean()
+
+
+def _bounce_rays(sph, idx, rng, mode):
+    """Origins on (or within a few ulp / ~pad/8 of) sphere idx's surface;
+    directions: the reference's scatter n + random_in_hemisphere(n), uniform,
+    or aimed at the silhouette of another sphere (tangent +- tiny)."""
+    n = len(idx)
+    c, r = sph[idx, :3], np.abs(sph[idx, 3])
+    u = rng.normal(size=(n, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    scale = max(1.0, float(np.max(np.abs(sph[:, :3]) + np.abs(sph[:, 3:4]))))
+    off = rng.choice([0.0, 1e-16, -1e-16, 1e-12, -1e-12, 2e-5 * scale / 64, -2e-5 * scale / 64], n)
+    o = c + (r * (1 + off))[:, None] * u
+    if mode == "scatter":
+        v = rng.uniform(-1, 1, (n, 3))
+        v /= np.maximum(1.0, np.linalg.norm(v, axis=1, keepdims=True))
+        v = np.where(((v * u).sum(1) > 0)[:, None], v, -v)
+        return o, u + v
+    if mode == "uniform":
+        return o, rng.normal(size=(n, 3))
+    k = rng.integers(0, len(sph), n)  # silhouette of sphere k seen from o
+    ck, rk = sph[k, :3], np.abs(sph[k, 3])
+    w = ck - o
+    w /= np.maximum(np.linalg.norm(w, axis=1, keepdims=True), 1e-300)
+    perp = rng.normal(size=(n, 3))
+    perp -= (perp * w).sum(1, keepdims=True) * w
+    perp /= np.maximum(np.linalg.norm(perp, axis=1, keepdims=True), 1e-300)
+    eps = rng.choice([0.0, 1e-12, -1e-12, 1e-7, -1e-7, 1e-4], n)
+    return o, (ck + (rk * (1 + eps))[:, None] * perp) - o
+
+
+def test_direction_maps_equal_linear(final_scene):
+    """Bounce rays with their previous hit as the hint (direction maps,
+    DESIGN.md §12): on every BVH sphere and on the ground near the field,
+    scatter / uniform / silhouette-grazing directions."""
+    rng = np.random.default_rng(77)
+    n = 300_000
+    for mode in ("scatter", "uniform", "silhouette"):
+        idx = rng.integers(0, len(final_scene), n)
+        idx[: n // 3] = 0  # the ground (a big sphere): its windowed patches
+        o, d = _bounce_rays(final_scene, idx, rng, mode)
+        if mode != "silhouette":  # ground points near the sphere field
+            m = idx == 0
+            g = np.stack([rng.uniform(-13, 13, m.sum()), np.zeros(m.sum()),
+                          rng.uniform(-13, 13, m.sum())], 1)
+            g[:, 1] = -1000.0 + np.sqrt(1000.0 ** 2 - g[:, 0] ** 2 - g[:, 2] ** 2)
+            o[m] = g
+            if mode == "scatter":  # n + random_in_hemisphere(n) about the ground normal
+                ng = (g - [0.0, -1000.0, 0.0]) / 1000.0
+                v = rng.uniform(-1, 1, (m.sum(), 3))
+                v /= np.maximum(1.0, np.linalg.norm(v, axis=1, keepdims=True))
+                v = np.where(((v * ng).sum(1) > 0)[:, None], v, -v)
+                d[m] = ng + v
+        _compare_hinted(final_scene, o, d, idx)
+
+
+def test_direction_maps_contact_scenes():
+    rng = np.random.default_rng(78)
+    base = np.concatenate([rng.uniform(-3, 3, (300, 3)), rng.uniform(0.05, 0.6, (300, 1))], 1)
+    scenes = {
+        "duplicates": np.concatenate([base, base[::-1]]),
+        "touching": np.array([[x, 0.0, z, 0.5] for x in range(-6, 7) for z in range(-6, 7)]),
+        "nested": np.concatenate([base, base * [1, 1, 1, 0.5], base * [1, 1, 1, 0.25]]),
+        "mixed_big": np.concatenate([base, [[0, -1000, 0, 1000], [0, 0, 0, 40.0],
+                                            [5, 5, 5, 1e-9]]]),
+        "negative_r": base * [1, 1, 1, -1],
+        "sparse": np.concatenate([rng.uniform(-40, 40, (60, 3)), rng.uniform(0.2, 1.0, (60, 1))], 1),
+    }
+    for name, sph in scenes.items():
+        for mode in ("scatter", "uniform", "silhouette"):
+            idx = rng.integers(0, len(sph), 60_000)
+            o, d = _bounce_rays(sph, idx, rng, mode)
+            _compare_hinted(sph, o, d, idx)
+
+
 def test_far_origins_inside_a_huge_ground():
     """Origins deep inside a ground sphere 10^4-10^5 scene scales big, aimed
     at small spheres half sunk into its surface: the FP32 grid query is not
