@@ -8,9 +8,15 @@ A step is one full frame of the configured workload: every rank renders its
 interleaved rows (psrt_camera_lists + psrt_trace + psrt_reduce through
 rt_render_device, inputs resident in HBM) and quantises them (write_color,
 color.h:8-24, per pixel); the uint8 rows are gathered to rank 0 over RCCL
-(--gather-fp64: the FP64 accumulators, quantised on rank 0). Total work is
-fixed as N grows ("strong" scaling). Rank 0 prints one JSON line; value =
-W*H*spp*K / wall, wall = max over ranks between barriers.
+(--gather-fp64: the FP64 accumulators, quantised on rank 0). Rank 0 prints
+one JSON line; value = W*H*spp*K / wall, wall = max over ranks between
+barriers.
+
+Scaling (--scaling): "weak" (default) keeps each GPU's work fixed: on N GPUs
+the frame is the configured W x H at N x spp, rows interleaved, so every rank
+renders the configured frame's sample count (C3: 96 M samples per GPU; the
+8-GPU frame is 1200x800 at 800 spp). "strong" renders the configured frame
+itself on any N.
 
 Default workload (BASELINE.json north star, configs[2]): the final
 random-spheres scene (485 spheres), 1200x800, 100 spp, depth 50.
@@ -89,6 +95,9 @@ def parse():
                     help="frames in flight (1 = each frame waits for the previous one; "
                          "0 = auto: 1 for multi-chunk frames, 3 for per-rank frames of "
                          "<= 32 M samples, else 2)")
+    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
+                    help="weak: N GPUs render the frame at N x spp (per-GPU work fixed); "
+                         "strong: the configured frame on any N")
     ap.add_argument("--emulate-shard", default="",
                     help="R/G: one process renders only rank R's rows of a G-GPU run "
                          "(per-rank step time of the multi-GPU bench, on one GPU; "
@@ -222,6 +231,10 @@ def main():
 
     w, h, spp = cfg["width"], cfg["height"], cfg["spp"]
     spheres, cam = scene_of(cfg)
+    # weak scaling: N GPUs (or an emulated shard of G) render N x spp
+    n_shards = int(args.emulate_shard.split("/")[1]) if args.emulate_shard else world
+    if args.scaling == "weak":
+        spp *= n_shards
     # Frames in flight: each slot has its own context (work queue, sample
     # buffer, stats), stream and output rows, so frame k+1 fills the CUs that
     # frame k's last waves release (DESIGN.md §7 "Frame pipelining").
@@ -395,11 +408,12 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (procedural scene: final random-spheres, glibc srand(1); counter RNG seed 0)",
-            "config": {"workload": cfg["desc"], "config_id": args.config, "width": w,
+            "config": {"workload": cfg["desc"] + (f"; {n_shards} GPUs at {n_shards} x spp (weak scaling: {cfg['spp']} spp of work per GPU)" if args.scaling == "weak" and n_shards > 1 else ""),
+                       "config_id": args.config, "width": w,
                        "height": h, "spp": spp, "max_depth": args.max_depth, "spheres": n,
                        "parallelism": (f"emulated shard {args.emulate_shard} (rows {off}::{stride})"
                                        if args.emulate_shard else f"interleaved rows x{world}") + ((", RCCL FP64 framebuffer gather" if args.gather_fp64 else ", per-rank write_color + RCCL uint8 gather") if world > 1 else "")},

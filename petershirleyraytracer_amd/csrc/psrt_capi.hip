@@ -18,7 +18,6 @@
 
 #include "../../include/rt.h"
 #include "psrt_bvh.h"
-#include "psrt_dirmap.h"
 #include "psrt_error.h"
 #include "psrt_kernels.h"
 
@@ -95,10 +94,6 @@ struct rt_context {
   int* d_cell_items = nullptr;
   int* d_nb_word = nullptr;
   int* d_nb_items = nullptr;
-  int4* d_dm_desc = nullptr;      // direction maps (psrt_dirmap.h), or nullptr
-  unsigned* d_dm_bits = nullptr;
-  int dm_maps = 0;
-  double dm_ms = 0.0;             // time of the last map build (psrt_dir_maps)
   std::vector<rt_sphere> scene;   // the scene the structures were built for
   psrt::GridHost pgrid;  // point-location grid (host copy of the geometry)
   double pad = 0.0;
@@ -179,68 +174,6 @@ int default_device() {
   return e ? std::atoi(e) : 0;
 }
 
-// Direction maps (psrt_dirmap.h): planned on the host, bits
-// computed by psrt_dir_maps on the context's stream; synchronous, like the
-// rest of set_scene. Temporaries are freed before returning.
-int build_dirmaps(rt_context* c, const rt_sphere* sph, int n, const psrt::BvhHost& b) {
-  const psrt::DirMapHost dm = psrt::plan_dirmaps(sph, n, b);
-  if (dm.n_maps <= 0) return RT_OK;
-  double4* d_ball = nullptr;
-  int* d_excl = nullptr;
-  double* d_bins = nullptr;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  auto cleanup = [&]() {
-    (void)hipFree(d_ball);
-    (void)hipFree(d_excl);
-    (void)hipFree(d_bins);
-    if (e0) (void)hipEventDestroy(e0);
-    if (e1) (void)hipEventDestroy(e1);
-  };
-  auto fail = [&](hipError_t e, const char* what) {
-    cleanup();
-    return set_error(e == hipErrorOutOfMemory ? RT_E_NOMEM : RT_E_HIP, "direction maps: %s: %s",
-                     what, hipGetErrorString(e));
-  };
-  hipError_t e;
-  const size_t nm = (size_t)dm.n_maps;
-  if ((e = hipMalloc(&c->d_dm_desc, dm.desc.size() * sizeof(int32_t))) != hipSuccess) return fail(e, "malloc");
-  if ((e = hipMalloc(&c->d_dm_bits, nm * psrt::kDirWords * sizeof(unsigned))) != hipSuccess) return fail(e, "malloc");
-  if ((e = hipMalloc(&d_ball, nm * sizeof(double4))) != hipSuccess) return fail(e, "malloc");
-  if ((e = hipMalloc(&d_excl, nm * sizeof(int))) != hipSuccess) return fail(e, "malloc");
-  if ((e = hipMalloc(&d_bins, dm.bins.size() * sizeof(double))) != hipSuccess) return fail(e, "malloc");
-  if ((e = hipMemcpy(c->d_dm_desc, dm.desc.data(), dm.desc.size() * sizeof(int32_t),
-                     hipMemcpyHostToDevice)) != hipSuccess) return fail(e, "copy");
-  if ((e = hipMemcpy(d_ball, dm.ball.data(), nm * sizeof(double4), hipMemcpyHostToDevice)) != hipSuccess)
-    return fail(e, "copy");
-  if ((e = hipMemcpy(d_excl, dm.excl.data(), nm * sizeof(int), hipMemcpyHostToDevice)) != hipSuccess)
-    return fail(e, "copy");
-  if ((e = hipMemcpy(d_bins, dm.bins.data(), dm.bins.size() * sizeof(double),
-                     hipMemcpyHostToDevice)) != hipSuccess) return fail(e, "copy");
-  psrt::DirMapArgs a{};
-  a.ball = d_ball;
-  a.excl = d_excl;
-  a.bins = d_bins;
-  a.leaf_geo = c->d_leaf_geo;
-  a.leaf_idx = c->d_leaf_idx;
-  a.n_leaf = c->n_leaf;
-  a.n_maps = dm.n_maps;
-  a.pad = c->pad;
-  a.bits = c->d_dm_bits;
-  if ((e = hipEventCreate(&e0)) != hipSuccess || (e = hipEventCreate(&e1)) != hipSuccess)
-    return fail(e, "event");
-  (void)hipEventRecord(e0, c->stream);
-  hipLaunchKernelGGL(psrt::psrt_dir_maps, dim3((unsigned)dm.n_maps), dim3(64), 0, c->stream, a);
-  if ((e = hipGetLastError()) != hipSuccess) return fail(e, "launch");
-  (void)hipEventRecord(e1, c->stream);
-  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return fail(e, "build");
-  float ms = 0.f;
-  (void)hipEventElapsedTime(&ms, e0, e1);
-  c->dm_ms = ms;
-  c->dm_maps = dm.n_maps;
-  cleanup();
-  return RT_OK;
-}
-
 }  // namespace
 
 extern "C" {
@@ -312,8 +245,6 @@ int rt_context_destroy(rt_context* c) {
   (void)hipFree(c->d_cell_items);
   (void)hipFree(c->d_nb_word);
   (void)hipFree(c->d_nb_items);
-  (void)hipFree(c->d_dm_desc);
-  (void)hipFree(c->d_dm_bits);
   for (auto e : c->ev) (void)hipEventDestroy(e);
   if (c->ev_all0) (void)hipEventDestroy(c->ev_all0);
   if (c->ev_all1) (void)hipEventDestroy(c->ev_all1);
@@ -377,9 +308,6 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
   (void)hipFree(c->d_cell_items);
   (void)hipFree(c->d_nb_word);
   (void)hipFree(c->d_nb_items);
-  (void)hipFree(c->d_dm_desc);
-  (void)hipFree(c->d_dm_bits);
-  c->d_dm_desc = nullptr, c->d_dm_bits = nullptr, c->dm_maps = 0;
   c->d_nodes = nullptr, c->d_leaf_geo = nullptr, c->d_leaf_idx = nullptr, c->d_big = nullptr;
   c->d_cell_start = nullptr, c->d_cell_items = nullptr;
   c->d_nb_word = nullptr, c->d_nb_items = nullptr;
@@ -422,8 +350,6 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
     if (!b.nb_items.empty())
       HIP_TRY(hipMemcpy(c->d_nb_items, b.nb_items.data(), b.nb_items.size() * sizeof(int),
                         hipMemcpyHostToDevice));
-    const int rc = build_dirmaps(c, sph, n, b);
-    if (rc) return rc;
   }
   c->scene.assign(sph, sph + n);
   return RT_OK;
@@ -444,8 +370,6 @@ static psrt::BvhView bvh_view(const rt_context* c) {
   v.nb_word = c->d_nb_word;
   v.nb_items = c->d_nb_items;
   v.nb_c2 = 0.25 * c->pad * c->pad;
-  v.dm_desc = c->dm_maps > 0 ? c->d_dm_desc : nullptr;
-  v.dm_bits = c->d_dm_bits;
   if (std::getenv("PSRT_NO_NEIGHBORS")) v.nb_c2 = -1.0;  // A/B knob: C^2 <= -r^2 never holds
   // grid bounds / scale in FP32, as used: the cell index of the device is a
   // function of these exact float values, and the host places each sphere in
@@ -615,9 +539,6 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     const char* e = std::getenv("PSRT_BATCH");  // tuning knob (default 24 of 64 lanes)
     ta.batch = e ? (unsigned)std::atoi(e) : 24u;
     if (ta.batch < 1) ta.batch = 1;
-    const char* db = std::getenv("PSRT_DM_BATCH");  // tuning knob (default 12 of 64 lanes)
-    ta.dm_batch = db ? (unsigned)std::atoi(db) : 12u;
-    if (ta.dm_batch < 1) ta.dm_batch = 1;
     const char* f = std::getenv("PSRT_RNG_FILL");  // tuning knob (default 2)
     ta.rng_fill = f ? std::atoi(f) : 2;
     if (ta.rng_fill < 1) ta.rng_fill = 1;
@@ -781,23 +702,21 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   c->last.kernel_ms = kms;
   c->last.total_ms = all;
   if (std::getenv("PSRT_STAMPS")) {
-    unsigned long long sec[54];
+    unsigned long long sec[50];
     HIP_TRY(hipMemcpy(sec, c->d_counters + 8, sizeof sec, hipMemcpyDeviceToHost));
-    static const char* names[21] = {"refill", "store", "hit", "hint", "nb", "cam",
+    static const char* names[19] = {"refill", "store", "hit", "hint", "nb", "cam",
                                     "grid", "walk", "trial", "scatter", "hint_hit",
                                     "hint_tiny", "grid_cell", "grid_out", "grid_none_fin",
-                                    "grid_none_inf", "far_miss", "park", "dirmap", "dir_clear",
-                                    "list_trip"};
+                                    "grid_none_inf", "far_miss", "park", "list_trip"};
     std::string u = "{\"psrt_util\": {";
-    for (int k = 0; k < 21; ++k) {
+    for (int k = 0; k < 19; ++k) {
       char b[128];
       const double w = (double)sec[12 + 2 * k], l = (double)sec[13 + 2 * k];
       std::snprintf(b, sizeof b, "%s\"%s\": [%.4g, %.2f]", k ? ", " : "", names[k], w,
                     w > 0 ? l / w : 0.0);
       u += b;
     }
-    std::fprintf(stderr, "%s}, \"dirmap_maps\": %d, \"dirmap_build_ms\": %.3f}\n", u.c_str(),
-                 c->dm_maps, c->dm_ms);
+    std::fprintf(stderr, "%s}}\n", u.c_str());
     if (c->d_wave_log && c->wave_log_used) {
       // wave timeline of the last launch: start, queue-empty and exit times
       // relative to the first start, percentiles over waves, in microseconds

@@ -55,7 +55,6 @@ struct TraceArgs {
                                     // iterations at queue empty, at exit} (s_memrealtime,
                                     // 100 MHz), or nullptr
   unsigned batch;                   // parked lanes that trigger a batched BVH pass
-  unsigned dm_batch;                // parked lanes that trigger a direction-map check
   int rng_fill;                     // look-ahead trials per lane per iteration (min)
   int rng_extra;                    // extra trials while a scattering lane has none queued
   unsigned refill_min;              // idle lanes that trigger the finish + refill block
@@ -85,10 +84,6 @@ struct BvhView {
   const int* __restrict__ nb_word;
   const int* __restrict__ nb_items;
   double nb_c2;  // (pad/2)^2: C <= 0 or C^2 <= nb_c2 * r^2 puts o in j's padded ball
-  // direction maps (psrt_dirmap.h), or nullptr: per (sphere, face) {first map
-  // or -1, M, i0 | j0 << 16, ni | nj << 16}; kDirWords bits words per map
-  const int4* __restrict__ dm_desc;
-  const unsigned* __restrict__ dm_bits;
 };
 
 constexpr int kCamTile = 8;         // camera-list tiles are 8 x 8 pixels (one wave)
@@ -104,19 +99,6 @@ struct CamListArgs {
   int n_leaf;
   double pad;                            // BVH box padding (absolute)
   uint4* __restrict__ plist;             // [rows * width]
-};
-
-// psrt_dir_maps: one wave per map; bit b of a map is set when no BVH sphere
-// (other than excl) can be met from the origin ball in direction bin b.
-struct DirMapArgs {
-  const double4* __restrict__ ball;      // per map: centre, radius
-  const int* __restrict__ excl;          // per map: sphere excluded (the origin's own), or -1
-  const double* __restrict__ bins;       // per bin: axis, cos(half), sin(half), 3 x pad
-  const double4* __restrict__ leaf_geo;  // BVH spheres {cx, cy, cz, r*r}
-  const int* __restrict__ leaf_idx;      // original index per BVH sphere
-  int n_leaf, n_maps;
-  double pad;                            // BVH pad: the root error budget of a hit point
-  unsigned* __restrict__ bits;           // [n_maps][kDirWords]
 };
 
 struct ReduceArgs {
@@ -135,7 +117,6 @@ __global__ void psrt_trace(const double4* __restrict__ geo, const double* __rest
                            double* __restrict__ samples, TraceArgs a, BvhView bv);
 __global__ void psrt_reduce(ReduceArgs a);
 __global__ void psrt_camera_lists(CamListArgs a);
-__global__ void psrt_dir_maps(DirMapArgs a);
 __global__ void psrt_quantize(const double* __restrict__ accum, unsigned char* __restrict__ rgb8,
                               unsigned n, int spp);
 __global__ void psrt_probe_hit(const double4* __restrict__ geo, const double* __restrict__ inv_r,

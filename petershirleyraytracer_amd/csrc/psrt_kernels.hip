@@ -24,7 +24,6 @@
 #include <stdint.h>
 
 #include "psrt_device.h"
-#include "psrt_dirmap.h"
 #include "psrt_kernels.h"
 
 #ifndef PSRT_ABLATE
@@ -58,7 +57,7 @@ enum Util { kURefill = 0, kUStore, kUHit, kUHint, kUNb, kUCam, kUGrid, kUWalk, k
             kUScatter,
             // hit_quick outcomes (lanes per wave execution, counted where decided)
             kUHintHit, kUHintTiny, kUGridCell, kUGridOut, kUGridNoneFin, kUGridNoneInf,
-            kUFarMiss, kUPark, kUDirMap, kUDirClear, kUListTrip, kUCount };
+            kUFarMiss, kUPark, kUListTrip, kUCount };
 
 __device__ __forceinline__ bool first_active_lane();
 
@@ -430,32 +429,6 @@ __device__ __forceinline__ bool first_active_lane() {
   return __lane_id() == (unsigned)__builtin_ctzll(__ballot(1));
 }
 
-// Cube-map cell of a vector (psrt_dirmap.h): face f = 2 * dominant axis + (its
-// sign < 0); (su, sv) = the other two coordinates over |dominant|. FP32: the
-// host widens every cell past this rounding (kDirEps). Callers keep the
-// dominant component normal (|v| far from FP32 under/overflow).
-__device__ __forceinline__ int cube_face(float x, float y, float z, float& su, float& sv) {
-  const float ax = __builtin_fabsf(x), ay = __builtin_fabsf(y), az = __builtin_fabsf(z);
-  int f;
-  float am;
-  if (ax >= ay && ax >= az) {
-    f = x < 0.0f, am = ax, su = y, sv = z;
-  } else if (ay >= az) {
-    f = 2 + (y < 0.0f), am = ay, su = x, sv = z;
-  } else {
-    f = 4 + (z < 0.0f), am = az, su = x, sv = y;
-  }
-  const float inv = __builtin_amdgcn_rcpf(am);  // v_rcp_f32 (1 ulp), inside kDirEps
-  su *= inv;
-  sv *= inv;
-  return f;
-}
-
-// floor((s + 1) / 2 * M) clamped to [0, M): hm = M / 2, top = M - 1
-__device__ __forceinline__ int cube_idx(float s, float hm, float top) {
-  return (int)fminf(fmaxf(__builtin_floorf((s + 1.0f) * hm), 0.0f), top);
-}
-
 // Cheap part of hittable_list::hit with culling: the previous-hit sphere
 // first, the big spheres, then the point-location grid. Returns true when the
 // closest hit is decided (bt, bi); false when the BVH must be walked (the
@@ -601,39 +574,6 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
   return false;
 }
 
-// Direction map of a parked bounce ray: o within pad/2 of the
-// hint sphere's surface (C^2 <= (pad/2)^2 r^2, C as sphere.cc:11 forms it),
-// in patch P; if the map of P has the bit of d's direction bin, no BVH sphere
-// other than the hint can have a root t >= 0, and the exact tests hit_quick
-// already made (hint, big spheres) decide the record. A in (1e-30, 1e30)
-// keeps d's dominant component normal in FP32. Called for a batch of parked
-// lanes at once (the bits load is one round trip per batch).
-__device__ __forceinline__ bool dir_map_clear(const BvhView& bv, const double4* __restrict__ lgeo,
-                                              double nb_c2, int hint, double ox, double oy,
-                                              double oz, double dx, double dy, double dz,
-                                              double A) {
-  if (hint < 0 || !(A > 1e-30 && A < 1e30)) return false;
-  const double4 sh = lgeo[hint];
-  const double ax = ox - sh.x, ay = oy - sh.y, az = oz - sh.z;
-  const double c = ((ax * ax + ay * ay) + az * az) - sh.w;
-  if (!(c * c <= nb_c2 * sh.w)) return false;
-  float su, sv;
-  const int pf = cube_face((float)ax, (float)ay, (float)az, su, sv);
-  const int4 dsc = bv.dm_desc[hint * 6 + pf];
-  if (dsc.x < 0) return false;
-  const float hm = 0.5f * (float)dsc.y, top = (float)(dsc.y - 1);
-  const int pi = cube_idx(su, hm, top) - (dsc.z & 0xFFFF);
-  const int pj = cube_idx(sv, hm, top) - (int)((unsigned)dsc.z >> 16);
-  const int nj = (int)((unsigned)dsc.w >> 16);
-  if ((unsigned)pi >= (unsigned)(dsc.w & 0xFFFF) || (unsigned)pj >= (unsigned)nj) return false;
-  float du, dv;
-  const int df = cube_face((float)dx, (float)dy, (float)dz, du, dv);
-  constexpr float bh = 0.5f * kDirN, btop = kDirN - 1;
-  const int bin = (df * kDirN + cube_idx(du, bh, btop)) * kDirN + cube_idx(dv, bh, btop);
-  const unsigned w = bv.dm_bits[(dsc.x + pi * nj + pj) * kDirWords + (bin >> 5)];
-  return (w >> (bin & 31)) & 1u;
-}
-
 // Entry t in [0, tmax] of the ray into the padded BVH root box, in FP64;
 // negative if the segment misses the box.
 __device__ __forceinline__ double root_box_entry(const BvhView& bv, double ox, double oy,
@@ -771,8 +711,7 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
   SectionClock<false> noclk;
   const GridC gc = grid_consts(bv);
   if (!hit_quick(geo, geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs, noclk, trapped,
-                 0u, bv.nb_word, gc) &&
-      !(bv.dm_desc && dir_map_clear(bv, geo, bv.nb_c2, hint, ox, oy, oz, dx, dy, dz, A)))
+                 0u, bv.nb_word, gc))
   {
     int node = 0;
     hit_traverse<false, false>(bv, bv.nodes, bv.leaf_idx, geo, hint, ox, oy, oz, dx, dy, dz, A,
@@ -891,7 +830,6 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   unsigned rays = 0;
   int hint = -1;  // sphere the ray starts on (the previous hit), tested first
   bool pending = false;  // parked for the next batched BVH pass
-  bool dm_seen = false;  // parked ray already checked against the direction maps
   int wnode = 0;         // where the parked ray's walk resumes
   bool sc_wait = false;  // hit resolved (pbi, pbt), scatter waits for a queued trial
   // look-ahead of random_in_unit_sphere (vec3.h:83-95): accepted trials, in
@@ -1069,7 +1007,6 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
           resolved = hit_quick(geo, lgeo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi,
                                cs, clk, trapped, q, lnb, gc);
           pending = !resolved;
-          dm_seen = false;
           wnode = 0;
           if (trapped && k < a.max_depth) {
             // the reference traces the max_depth - k rays that remain, all at
@@ -1095,28 +1032,6 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     }
     clk.mark(kSecHit);
     if constexpr (kBVH) {
-      // Direction maps for the lanes parked since the last
-      // check, together once a.dm_batch of them wait (or before a walk): a ray
-      // they clear is resolved here, the others stay parked for the walk.
-      if (bv.dm_desc) {
-        const uint64_t fresh = __ballot(pending && !dm_seen);
-        const uint64_t mv = __ballot(active && !pending);
-        if (fresh != 0 && ((unsigned)__popcll(fresh) >= a.dm_batch || mv == 0 ||
-                           (unsigned)__popcll(__ballot(pending)) >= a.batch)) {
-          if (pending && !dm_seen) {
-            clk.util(kUDirMap);
-            unsigned zg = 0;
-            asm volatile("" : "+v"(zg));
-            const GridC& gc = *(const GridC*)((const char*)&s_gc + zg);
-            if (dir_map_clear(bv, lgeo, gc.nb_c2, hint, ox, oy, oz, dx, dy, dz, A)) {
-              clk.util(kUDirClear);
-              pending = false;
-              resolved = true;
-            }
-            dm_seen = true;
-          }
-        }
-      }
       const uint64_t pend = __ballot(pending);
       const uint64_t movable = __ballot(active && !pending);
       if (pend != 0 && ((unsigned)__popcll(pend) >= a.batch || movable == 0)) {
@@ -1478,59 +1393,6 @@ __global__ __launch_bounds__(64) void psrt_camera_lists(CamListArgs a) {
     if (!full) w[0] = (w[0] & 0xFFFF0000u) | n;
   }
   a.plist[(size_t)rk * a.width + px] = make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-// ---- direction maps (psrt_dirmap.h) ---------------------------
-//
-// One wave per map, one bit per direction bin (bin = 64 p + lane). BVH sphere
-// k (padded ball, radius |r| + pad: an accepted root's hit point lies within
-// the root error of the surface) can be met by a ray from the origin ball
-// (m, rho) in a direction of bin b (cone: axis a_b, half-angle h_b) iff the
-// ball (c_k, R = |r| + pad + rho) meets the cone with apex m: L = |c_k - m|
-// <= R, or angle(a_b, c_k - m) <= h_b + asin(R / L). Compared through cosines
-// with R widened and a 1e-9 margin: the bit is clear whenever a meeting is
-// possible.
-__global__ __launch_bounds__(64) void psrt_dir_maps(DirMapArgs a) {
-  __shared__ double s_bin[kDirBins * 5];
-  const unsigned lane = threadIdx.x;
-  for (int e = lane; e < kDirBins; e += 64)
-    for (int q = 0; q < 5; ++q) s_bin[e * 5 + q] = a.bins[e * 8 + q];
-  __syncthreads();
-  const int map = blockIdx.x;
-  const double4 b = a.ball[map];
-  const int ex = a.excl[map];
-  constexpr int kPer = kDirBins / 64;
-  static_assert(kPer <= 32, "one mask bit per bin of a lane");
-  unsigned blocked = 0;
-  bool all = false;
-  for (int k = 0; k < a.n_leaf; ++k) {
-    if (a.leaf_idx[k] == ex) continue;
-    const double4 s = a.leaf_geo[k];
-    const double vx = s.x - b.x, vy = s.y - b.y, vz = s.z - b.z;
-    const double L2 = (vx * vx + vy * vy) + vz * vz;
-    const double R = (__builtin_sqrt(s.w) * (1.0 + 0x1p-40) + a.pad + b.w) * (1.0 + 0x1p-40);
-    if (!(L2 > R * R * (1.0 + 0x1p-30))) {  // the origin ball meets it (or NaN)
-      all = true;
-      break;
-    }
-    const double L = __builtin_sqrt(L2);
-    const double sg = R / L, cg = __builtin_sqrt(1.0 - sg * sg);
-#pragma unroll
-    for (int p = 0; p < kPer; ++p) {
-      const double* e = &s_bin[(p * 64 + lane) * 5];
-      const double thr = (e[3] * cg - e[4] * sg) - 1e-9;  // cos(h_b + asin(R/L)), lowered
-      const double dt = (e[0] * vx + e[1] * vy) + e[2] * vz;
-      if (dt >= thr * L) blocked |= 1u << p;
-    }
-  }
-#pragma unroll
-  for (int p = 0; p < kPer; ++p) {
-    const uint64_t m = __ballot(!all && !((blocked >> p) & 1u));
-    if (lane == 0) {
-      a.bits[(size_t)map * kDirWords + 2 * p] = (unsigned)m;
-      a.bits[(size_t)map * kDirWords + 2 * p + 1] = (unsigned)(m >> 32);
-    }
-  }
 }
 
 __global__ __launch_bounds__(256) void psrt_quantize(const double* __restrict__ accum,

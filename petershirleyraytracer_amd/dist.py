@@ -48,8 +48,14 @@ def gather_frame(local: torch.Tensor, height: int, rank: int, world: int,
     padded = local.new_zeros((max_rows, w, ch))
     if mine:
         padded[:mine] = local
-    parts = [torch.empty_like(padded) for _ in range(world)] if rank == dst else None
-    dist.gather(padded, parts, dst=dst)
+    # gloo's gather takes host tensors only (the N > 1 rehearsal on one GPU
+    # runs gloo over device frames): stage through host memory there
+    host = dist.get_backend() == "gloo" and padded.device.type != "cpu"
+    send = padded.cpu() if host else padded
+    parts = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
+    dist.gather(send, parts, dst=dst)
+    if host and rank == dst:
+        parts = [p.to(local.device) for p in parts]
     if rank != dst:
         return None
     frame = local.new_empty((height, w, ch))

@@ -102,7 +102,8 @@ def test_bvh_ties_and_degenerate_scenes():
 
 def _compare_hinted(sph, o, d, hint):
     """The trace kernel's bounce-ray call (previous hit as the hint: the
-    neighbour-list and direction-map paths) against the reference scan."""
+    hint-first test and the neighbour-list path) against the
+    reference scan."""
     rays = np.concatenate([o, d, np.zeros((len(o), 1)), np.full((len(o), 1), np.inf)], 1)
     a = world_hit(sph, rays, cull=True, hints=hint)
     b = world_hit(sph, rays, cull=False)
@@ -141,15 +142,15 @@ def _bounce_rays(sph, idx, rng, mode):
     return o, (ck + (rk * (1 + eps))[:, None] * perp) - o
 
 
-def test_direction_maps_equal_linear(final_scene):
-    """Bounce rays with their previous hit as the hint (direction maps,
-    DESIGN.md §12): on every BVH sphere and on the ground near the field,
-    scatter / uniform / silhouette-grazing directions."""
+def test_hinted_bounce_rays_equal_linear(final_scene):
+    """Bounce rays with their previous hit as the hint: on every BVH sphere
+    and on the ground near the field, scatter / uniform / silhouette-grazing
+    directions."""
     rng = np.random.default_rng(77)
     n = 300_000
     for mode in ("scatter", "uniform", "silhouette"):
         idx = rng.integers(0, len(final_scene), n)
-        idx[: n // 3] = 0  # the ground (a big sphere): its windowed patches
+        idx[: n // 3] = 0  # the ground (a big sphere: no neighbour list)
         o, d = _bounce_rays(final_scene, idx, rng, mode)
         if mode != "silhouette":  # ground points near the sphere field
             m = idx == 0
@@ -166,7 +167,7 @@ def test_direction_maps_equal_linear(final_scene):
         _compare_hinted(final_scene, o, d, idx)
 
 
-def test_direction_maps_contact_scenes():
+def test_hinted_bounce_rays_contact_scenes():
     rng = np.random.default_rng(78)
     base = np.concatenate([rng.uniform(-3, 3, (300, 3)), rng.uniform(0.05, 0.6, (300, 1))], 1)
     scenes = {
