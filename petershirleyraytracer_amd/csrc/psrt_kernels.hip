@@ -28,7 +28,13 @@
 
 #ifndef PSRT_ABLATE
 #define PSRT_ABLATE 0  // measurement builds: 1 = hit_quick twice, 2 = two trials per trial,
-                       // 3 = the BVH walk twice
+                       // 3 = the BVH walk twice; sub-sections of hit_quick twice: 4 = the hint
+                       // test, 5 = the big spheres, 6 = grid_locate, 7 = the candidate loop;
+                       // 8 = the refill's per-lane setup, 9 = the scatter
+#endif
+// Ablation: keep a measurement copy's results alive without storing them.
+#if PSRT_ABLATE
+#define PSRT_SINK(x) asm volatile("" ::"v"(x))
 #endif
 
 #ifndef PSRT_SLAB_ASM
@@ -331,13 +337,24 @@ constexpr int kGridNone = -1, kGridOutside = -2;
 // spill lane is a VALU v_readlane (~20 per grid query).
 struct GridC {
   float glo[3], ghi[3], ginv, gmargin;
-  int gdims[3], pad_;
+  int gdims[3], ncell;
+  // cell-index form of the widened segment bounds: fma(min, ginv, a0[k]) =
+  // (min - m - glo) ginv and fma(max, ginv, a1[k]) = (max + m - glo) ginv, up
+  // to FP32 rounding (~2^-24 of the coordinates, far inside the margin m)
+  float a0[3], a1[3];
+  int top[3], pad_;
   double r_check, nb_c2;
 };
 
 __device__ __forceinline__ GridC grid_consts(const BvhView& bv) {
   GridC g;
-  for (int k = 0; k < 3; ++k) g.glo[k] = bv.glo[k], g.ghi[k] = bv.ghi[k], g.gdims[k] = bv.gdims[k];
+  for (int k = 0; k < 3; ++k) {
+    g.glo[k] = bv.glo[k], g.ghi[k] = bv.ghi[k], g.gdims[k] = bv.gdims[k];
+    g.a0[k] = -(bv.glo[k] + bv.gmargin) * bv.ginv;
+    g.a1[k] = -(bv.glo[k] - bv.gmargin) * bv.ginv;
+    g.top[k] = bv.gdims[k] - 1;
+  }
+  g.ncell = bv.gdims[0] * bv.gdims[1] * bv.gdims[2];
   g.ginv = bv.ginv;
   g.gmargin = bv.gmargin;
   g.pad_ = 0;
@@ -346,17 +363,56 @@ __device__ __forceinline__ GridC grid_consts(const BvhView& bv) {
   return g;
 }
 
+#ifndef PSRT_GRID_INT
+#define PSRT_GRID_INT 1  // grid_locate on saturating floor-converts + integer clamps
+#endif
+
+// floor(x) as int, saturating (NaN -> 0): one v_cvt_flr_i32_f32
+__device__ __forceinline__ int cvt_flr_i32(float x) {
+  int r;
+  asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
+// min(max(x, 0), hi): one v_med3_i32
+__device__ __forceinline__ int clamp0_i32(int x, int hi) {
+  int r;
+  asm("v_med3_i32 %0, %1, 0, %2" : "=v"(r) : "v"(x), "v"(hi));
+  return r;
+}
+
 __device__ __forceinline__ int grid_locate(const GridC& bv, double ox, double oy, double oz,
                                            double dx, double dy, double dz, double bt) {
   if (!(bt < 1e30)) return kGridNone;
   // FP32 is enough within the caller's range guard: the test is conservative
   // and its error is inside pad + margin (psrt_bvh.cpp, hit_quick)
-  const float m = bv.gmargin;
   const float o3[3] = {(float)ox, (float)oy, (float)oz};
   const float d3[3] = {(float)dx, (float)dy, (float)dz};
   const float tb = (float)bt * 1.00000048f;
   int ci[3];
   bool outside = false, ok = true, one = true;
+#if PSRT_GRID_INT
+  // Cell range [c0, c1] of the widened segment per axis, from saturating
+  // floor-converts (huge coordinates saturate, and the caller's range guard
+  // keeps NaN out). Outside the grid when c1 < 0 or c0 > top on some axis:
+  // the widened bound then lies below glo / at or past the grid's far side
+  // (up to rounding far inside the margin), where no padded sphere box
+  // reaches. Then clipped to the grid: a hit point lies in a padded sphere
+  // box, hence in a cell of the grid.
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float e = __builtin_fmaf(tb, d3[k], o3[k]);
+    const int r0 = cvt_flr_i32(__builtin_fmaf(fminf(o3[k], e), bv.ginv, bv.a0[k]));
+    const int r1 = cvt_flr_i32(__builtin_fmaf(fmaxf(o3[k], e), bv.ginv, bv.a1[k]));
+    const int top = bv.top[k];
+    outside = outside || r1 < 0 || r0 > top;
+    const int c0 = clamp0_i32(r0, top), c1 = clamp0_i32(r1, top);
+    ok = ok && c1 - c0 <= 1;
+    one = one && c1 == c0;
+    ci[k] = c0;
+  }
+#else
+  const float m = bv.gmargin;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const float e = __builtin_fmaf(tb, d3[k], o3[k]);
@@ -373,11 +429,12 @@ __device__ __forceinline__ int grid_locate(const GridC& bv, double ox, double oy
     one = one && c1 == c0;
     ci[k] = c0;
   }
+#endif
   if (outside) return kGridOutside;
   if (!ok) return kGridNone;
   // one cell: its list; two cells on some axis: the 2x2x2 block list from ci
   const int cell = (ci[2] * bv.gdims[1] + ci[1]) * bv.gdims[0] + ci[0];
-  return one ? cell : cell + bv.gdims[0] * bv.gdims[1] * bv.gdims[2];
+  return one ? cell : cell + bv.ncell;
 }
 
 __device__ __forceinline__ float tmax_up(double t) {
@@ -478,6 +535,15 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     clk.util(kUHint);
     const double4 sh = lgeo[hint];
     double ch;
+#if PSRT_ABLATE == 4
+    {
+      double x0 = ox, bt2 = bt, ch2;
+      int bi2 = bi;
+      asm volatile("" : "+v"(x0));
+      test_sphere(sh, hint, x0, oy, oz, dx, dy, dz, A, bt2, bi2, &ch2);
+      PSRT_SINK(bt2); PSRT_SINK(bi2); PSRT_SINK(ch2);
+    }
+#endif
     test_sphere(sh, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, &ch);
     fix = bv.fixpoint && ch == 0.0 && sh.w >= 0x1p-700 && sh.w <= 0x1p700 && am <= 0x1p40;
     ++cs.spheres;
@@ -496,6 +562,19 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
       nbw = lnb[hint];
   }
   clk.mark(kSecQHint);
+#if PSRT_ABLATE == 5
+  {
+    double x0 = ox, bt2 = bt;
+    int bi2 = bi;
+    bool f2 = false;
+    asm volatile("" : "+v"(x0));
+    for (int b = 0; b < bv.n_big; ++b) {
+      const int idx = bv.big_idx[b];
+      if (idx != hint) f2 |= test_sphere(geo[idx], idx, x0, oy, oz, dx, dy, dz, A, bt2, bi2);
+    }
+    PSRT_SINK(bt2); PSRT_SINK(bi2); PSRT_SINK((int)f2);
+  }
+#endif
   for (int b = 0; b < bv.n_big; ++b) {
     const int idx = bv.big_idx[b];
     if (idx != hint) full |= test_sphere(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
@@ -527,6 +606,15 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     // sphere's padded box): coordinates up to ~630 S; admitted up to 256 S
     // (|o| <= 4 r_check, bt |d| <= 4 r_check), else the walk / root-box test
     const double rg = 4.0 * gc.r_check;
+#if PSRT_ABLATE == 6
+    {
+      double x0 = ox;
+      asm volatile("" : "+v"(x0));
+      const int c2 = (am <= rg && (bt * bt) * A <= rg * rg)
+                         ? grid_locate(gc, x0, oy, oz, dx, dy, dz, bt) : kGridNone;
+      PSRT_SINK(c2);
+    }
+#endif
     const int cell = (am <= rg && (bt * bt) * A <= rg * rg)
                          ? grid_locate(gc, ox, oy, oz, dx, dy, dz, bt) : kGridNone;
     listed = cell != kGridNone;
@@ -540,6 +628,28 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
       cnt = bv.cell_start[cell + 1] - e0;
     }
   }
+#if PSRT_ABLATE == 7
+  {
+    double x0 = ox, bt2 = bt;
+    int bi2 = bi;
+    bool f2 = false;
+    uint64_t lo2 = lo, hi2 = hi;
+    asm volatile("" : "+v"(x0));
+    for (int e = 0; e < cnt; ++e) {
+      int idx;
+      if (cam) {
+        lo2 = (lo2 >> 16) | (hi2 << 48);
+        hi2 >>= 16;
+        idx = (int)(lo2 & 0xFFFFu);
+      } else {
+        idx = items[e];
+      }
+      if (idx == hint) continue;
+      f2 |= test_sphere(lgeo[idx], idx, x0, oy, oz, dx, dy, dz, A, bt2, bi2);
+    }
+    PSRT_SINK(bt2); PSRT_SINK(bi2); PSRT_SINK((int)f2);
+  }
+#endif
   for (int e = 0; e < cnt; ++e) {
     clk.util(kUListTrip);
     int idx;
@@ -936,6 +1046,24 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
           const int j = rc.hm1_i - r;
           const unsigned pix = (unsigned)j * dw.d + i;
           const unsigned s = (unsigned)rc.s_begin + sl;
+#if PSRT_ABLATE == 8
+          {
+            unsigned u2 = (unsigned)unit;
+            asm volatile("" : "+v"(u2));
+            const unsigned q2 = fast_div(u2, ds), r2 = fast_div(q2, dw);
+            const unsigned i2 = q2 - r2 * dw.d;
+            const int j2 = rc.hm1_i - (rc.row_offset + (int)r2 * rc.row_stride);
+            uint64_t g2 = splitmix64((((uint64_t)((unsigned)j2 * dw.d + i2)) << 32 |
+                                      (uint64_t)(rc.s_begin + u2 - q2 * ds.d)) ^ rc.seedmix);
+            const double uu = ((double)i2 + random_double(g2)) / rc.wm1;
+            const double vv = ((double)j2 + random_double(g2)) / rc.hm1;
+            const double* cm = rc.cam;
+            const double ex = ((cm[3] + uu * cm[6]) + vv * cm[9]) - cm[0];
+            const double ey = ((cm[4] + uu * cm[7]) + vv * cm[10]) - cm[1];
+            const double ez = ((cm[5] + uu * cm[8]) + vv * cm[11]) - cm[2];
+            PSRT_SINK((ex * ex + ey * ey) + ez * ez); PSRT_SINK(g2);
+          }
+#endif
           rng = splitmix64((((uint64_t)pix) << 32 | (uint64_t)s) ^ rc.seedmix);
           // main.cc:80-81, camera.h:25-28
           const double u = ((double)i + random_double(rng)) / rc.wm1;
@@ -1123,6 +1251,18 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     sc_wait = want && qn == 0;
     if (want && qn > 0) {
       clk.util(kUScatter);
+#if PSRT_ABLATE == 9
+      {
+        double x0 = ox;
+        asm volatile("" : "+v"(x0));
+        const HitRec h2 = hit_record_of(lgeo[hit], linv[hit], t, x0, oy, oz, dx, dy, dz);
+        double sx = pm1_of(q0x), sy = pm1_of(q0y), sz = pm1_of(q0z);
+        if (!((sx * h2.nx + sy * h2.ny) + sz * h2.nz > 0.0)) sx = -sx, sy = -sy, sz = -sz;
+        const double ex = ((h2.px + h2.nx) + sx) - h2.px, ey = ((h2.py + h2.ny) + sy) - h2.py,
+                     ez = ((h2.pz + h2.nz) + sz) - h2.pz;
+        PSRT_SINK((ex * ex + ey * ey) + ez * ez);
+      }
+#endif
       const HitRec h = hit_record_of(lgeo[hit], linv[hit], t, ox, oy, oz, dx, dy, dz);
       // vec3.h:78-81 random(-1, 1) from the queued draws; vec3.h:102-109 flip
       double rx = pm1_of(q0x), ry = pm1_of(q0y), rz = pm1_of(q0z);
