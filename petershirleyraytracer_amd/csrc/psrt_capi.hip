@@ -84,6 +84,7 @@ struct rt_context {
   int cus = 0;
   int grid = 0;       // resident blocks of psrt_trace<false>
   int grid_bvh = 0;   // resident blocks of psrt_trace<true>
+  unsigned lds_max = 0;  // largest dynamic LDS that keeps grid_bvh resident (staged scenes)
   // exact-culling structure (psrt_bvh.h)
   bool bvh = false;
   float4* d_nodes = nullptr;
@@ -214,9 +215,20 @@ int rt_context_create(int device, rt_context** out) {
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace<false, false, false>,
                                                         psrt::kTraceBlock, 0));
   c->grid = c->cus * (per_cu < 1 ? 1 : per_cu);
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace<true, false, true>,
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace<true, false, false>,
                                                         psrt::kTraceBlock, 0));
   c->grid_bvh = c->cus * (per_cu < 1 ? 1 : per_cu);
+  // the staged-scene variant keeps that residency up to lds_max bytes of
+  // dynamic LDS (largest multiple of 256 B the occupancy query accepts)
+  for (unsigned b = 65536; b >= 256; b -= 256) {
+    int pc = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, psrt::psrt_trace<true, false, true>,
+                                                     psrt::kTraceBlock, b) == hipSuccess &&
+        pc >= per_cu) {
+      c->lds_max = b;
+      break;
+    }
+  }
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIP_TRY(hipMalloc(&c->d_counters, 64 * sizeof(unsigned long long)));
   HIP_TRY(hipEventCreate(&c->ev_all0));
@@ -320,11 +332,20 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
     c->r_check = b.r_check;
     std::vector<double4> lg(c->n_leaf);
     for (int k = 0; k < c->n_leaf; ++k) lg[k] = geo[b.leaf_idx[k]];
-    HIP_TRY(hipMalloc(&c->d_nodes, b.nodes.size() * sizeof(psrt::BvhNode)));
+    HIP_TRY(hipMalloc(&c->d_nodes, b.nodes.size() * sizeof(psrt::DevNode)));
     HIP_TRY(hipMalloc(&c->d_leaf_geo, (size_t)c->n_leaf * sizeof(double4)));
     HIP_TRY(hipMalloc(&c->d_leaf_idx, (size_t)c->n_leaf * sizeof(int)));
     HIP_TRY(hipMalloc(&c->d_big, (size_t)(c->n_big > 0 ? c->n_big : 1) * sizeof(int)));
-    HIP_TRY(hipMemcpy(c->d_nodes, b.nodes.data(), b.nodes.size() * sizeof(psrt::BvhNode),
+    std::vector<psrt::DevNode> dn(b.nodes.size());
+    for (size_t k = 0; k < dn.size(); ++k) {
+      const psrt::BvhNode& nd = b.nodes[k];
+      float sk, lf;
+      std::memcpy(&sk, &nd.skip, 4);
+      std::memcpy(&lf, &nd.leaf, 4);
+      dn[k].xy = make_float4(nd.lo[0], nd.lo[1], nd.hi[0], nd.hi[1]);
+      dn[k].z = make_float4(nd.lo[2], nd.hi[2], sk, lf);
+    }
+    HIP_TRY(hipMemcpy(c->d_nodes, dn.data(), dn.size() * sizeof(psrt::DevNode),
                       hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_leaf_geo, lg.data(), lg.size() * sizeof(double4),
                       hipMemcpyHostToDevice));
@@ -629,14 +650,16 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     const double4* g4 = c->d_geo;
     const double* ir = c->d_inv_r;
     const dim3 blk(psrt::kTraceBlock);
-    const bool lds = c->n_nodes + 1 <= psrt::kLdsNodes && c->n <= psrt::kLdsSpheres &&
-                     c->n_leaf <= psrt::kLdsSpheres &&
-                     !std::getenv("PSRT_NO_LDS");
+    // scene data in LDS when three workgroups per CU still fit (the BVH
+    // kernel's resident count otherwise: its global-memory variant)
+    const unsigned lds_bytes = psrt::lds_layout(c->n, c->n_nodes, c->n_leaf).bytes;
+    const bool lds = use_bvh && lds_bytes <= c->lds_max && !std::getenv("PSRT_NO_LDS");
     // PSRT_BLOCKS_PER_CU: measurement knob (occupancy sweep), default = resident max
     const char* bpc = std::getenv("PSRT_BLOCKS_PER_CU");
     auto launch = [&](auto kern, int grid) {
       if (bpc) grid = std::min(grid, std::max(1, c->cus * std::atoi(bpc)));
-      hipLaunchKernelGGL(kern, dim3(grid), blk, 0, st, g4, ir, c->d_samples, ta, bv);
+      hipLaunchKernelGGL(kern, dim3(grid), blk, lds ? lds_bytes : 0, st, g4, ir, c->d_samples, ta,
+                         bv);
     };
     if (!use_bvh)
       stamps ? launch(psrt::psrt_trace<false, true, false>, c->grid)

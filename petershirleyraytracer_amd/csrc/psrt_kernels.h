@@ -6,15 +6,35 @@
 
 namespace psrt {
 
-constexpr int kTraceBlock = 512;     // 8 waves per workgroup (3 per CU share 160 KB of LDS)
+#ifndef PSRT_TRACE_BLOCK
+#define PSRT_TRACE_BLOCK 512  // 8 waves per workgroup (3 per CU share 160 KB of LDS)
+#endif
+constexpr int kTraceBlock = PSRT_TRACE_BLOCK;
 #ifndef PSRT_WORK_CHUNK
 #define PSRT_WORK_CHUNK 1024  // 512 before frame pipelining (C3 pipelined 16.00 -> 15.85 ms)
 #endif
 constexpr unsigned kWorkChunk = PSRT_WORK_CHUNK;  // largest queue ticket (units); see queue_phases
 constexpr unsigned kLinearChunk = 1024;           // queue ticket of the small-scene (linear) path
 constexpr int kQueuePhases = 5;        // guided: ticket sizes halve toward the end, >= 64
-constexpr int kLdsNodes = 640;         // BVH nodes staged per workgroup (20 KB of LDS)
-constexpr int kLdsSpheres = 640;       // spheres staged per workgroup (25 KB of LDS)
+// Scene data psrt_trace stages in (dynamic) LDS per workgroup: BVH nodes (2
+// float4 each, plus the padding node), spheres {c, r*r}, 1/r, leaf slots and
+// neighbour words; byte offsets, 16-B aligned. The host stages them when as
+// many workgroups per CU stay resident as without (C3: 573 nodes, 485
+// spheres, 41.6 KB; three workgroups, and psrt_reduce's 22 KB beside them).
+struct LdsLayout {
+  unsigned nodes, geo, inv, leaf, nb, bytes;
+};
+__host__ __device__ inline LdsLayout lds_layout(int n, int n_nodes, int n_leaf) {
+  auto a16 = [](unsigned x) { return (x + 15u) & ~15u; };
+  LdsLayout l;
+  l.nodes = 0;
+  l.geo = 32u * (unsigned)(n_nodes + 1);
+  l.inv = l.geo + 32u * (unsigned)n;
+  l.leaf = a16(l.inv + 8u * (unsigned)n);
+  l.nb = a16(l.leaf + 4u * (unsigned)n_leaf);
+  l.bytes = a16(l.nb + 4u * (unsigned)n);
+  return l;
+}
 
 // Division of n < 2^32 by an invariant d: q = (t + ((n - t) >> sh1)) >> sh2,
 // t = mulhi(m, n) (host: FastDiv::make).
@@ -63,8 +83,16 @@ struct TraceArgs {
   unsigned flush_at;                // per-lane counters flush to the totals at this value
 };
 
+// BVH node as the device reads it (two float4, from psrt_bvh.h BvhNode):
+// {lo.x, lo.y, hi.x, hi.y}, {lo.z, hi.z, skip, leaf} (skip / leaf: int bits),
+// so the slab test's coordinate pairs are adjacent (packed FP32 FMAs).
+struct DevNode {
+  float4 xy, z;
+};
+static_assert(sizeof(DevNode) == 32, "device node layout");
+
 struct BvhView {
-  const float4* __restrict__ nodes;      // 2 x float4 per node: {lo, skip}, {hi, leaf}
+  const float4* __restrict__ nodes;      // DevNode as 2 x float4
   const double4* __restrict__ leaf_geo;  // sphere per leaf slot
   const int* __restrict__ leaf_idx;      // original index per leaf slot
   const int* __restrict__ big_idx;       // spheres tested on every ray

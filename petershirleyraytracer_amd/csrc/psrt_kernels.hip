@@ -37,6 +37,10 @@
 #define PSRT_SINK(x) asm volatile("" ::"v"(x))
 #endif
 
+#ifndef PSRT_SLAB_PK
+#define PSRT_SLAB_PK 0  // 1: slab-test FMAs as packed FP32 pairs (-2% VALU, yet 1% slower)
+#endif
+
 #ifndef PSRT_SLAB_ASM
 #define PSRT_SLAB_ASM 1  // slab test min/max as inline asm (no per-box NaN canonicalisation)
 #endif
@@ -298,6 +302,10 @@ __device__ __forceinline__ HitRec hit_record_of(const double4 s, double ir, doub
 // nearer the surface always take the full test.
 // Returns false when the pre-reject decided the sphere, true when the full
 // test ran. *c_out (if given) receives C = amc.amc - r^2 as sphere.cc:11 forms it.
+#ifndef PSRT_PRE2
+#define PSRT_PRE2 0  // 1: pre-reject as one comparison (max of the two bounds): measured +1% VALU
+#endif
+
 __device__ __forceinline__ bool test_sphere(const double4 s, int idx, double ox, double oy,
                                             double oz, double dx, double dy, double dz,
                                             double A, double& best_t, int& best_i,
@@ -305,11 +313,23 @@ __device__ __forceinline__ bool test_sphere(const double4 s, int idx, double ox,
   const double ax = ox - s.x, ay = oy - s.y, az = oz - s.z;
   const double c = ((ax * ax + ay * ay) + az * az) - s.w;
   if (c_out) *c_out = c;
+#if PSRT_PRE2
+  // the same two conditions as one comparison, strict:
+  // C^2 > max(2^-34 (C + r^2), best_t^2 A (1 + 2^-4)) k2 (best_t = inf: never);
+  // k2 by one FMA (a bound of ours, not reference arithmetic: its rounding is
+  // ~2^-52, far inside the 2^-4 and 2^-33 margins)
+  if (c > 0.0) {
+    const double k2 = 2.0 * __builtin_fma(2.0, s.w, c);
+    const double m = __builtin_fmax(0x1p-34 * (c + s.w), (best_t * best_t) * A * (1.0 + 0x1p-4));
+    if (c * c > m * k2) return false;
+  }
+#else
   if (c > 0.0 && best_t < 1e100) {
     const double c2 = c * c, k2 = 2.0 * (c + 2.0 * s.w);
     if (c2 >= 0x1p-34 * (c + s.w) * k2 && (best_t * best_t) * A * k2 * (1.0 + 0x1p-4) < c2)
       return false;
   }
+#endif
   const double hb = (dx * ax + dy * ay) + dz * az;
   const double disc = hb * hb - A * c;
   if (disc < 0.0) return true;
@@ -447,13 +467,26 @@ __device__ __forceinline__ float safe_inv(float d) {
   return __builtin_amdgcn_rcpf(m);  // v_rcp_f32 (1 ulp): the padded boxes absorb it
 }
 
-// Conservative FP32 ray-box test over [tlo, tmax] (boxes padded, psrt_bvh.cpp).
-__device__ __forceinline__ bool slab_hit(const float4 lo, const float4 hi, float ix, float iy,
+// Conservative FP32 ray-box test over [tlo, tmax] (boxes padded, psrt_bvh.cpp)
+// of a device node (psrt_kernels.h DevNode): n0 = {lo.x, lo.y, hi.x, hi.y},
+// n1 = {lo.z, hi.z, skip, leaf}.
+__device__ __forceinline__ bool slab_hit(const float4 n0, const float4 n1, float ix, float iy,
                                          float iz, float oix, float oiy, float oiz, float tlo,
                                          float tmax) {
-  const float x0 = __builtin_fmaf(lo.x, ix, -oix), x1 = __builtin_fmaf(hi.x, ix, -oix);
-  const float y0 = __builtin_fmaf(lo.y, iy, -oiy), y1 = __builtin_fmaf(hi.y, iy, -oiy);
-  const float z0 = __builtin_fmaf(lo.z, iz, -oiz), z1 = __builtin_fmaf(hi.z, iz, -oiz);
+#if PSRT_SLAB_PK
+  // packed FP32 (v_pk_fma_f32, two FMAs per issue) on the node's coordinate
+  // pairs: (x0, y0), (x1, y1), (z0, z1)
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 ixy = {ix, iy}, oxy = {-oix, -oiy};
+  const f2 txy0 = __builtin_elementwise_fma((f2){n0.x, n0.y}, ixy, oxy);
+  const f2 txy1 = __builtin_elementwise_fma((f2){n0.z, n0.w}, ixy, oxy);
+  const f2 tz = __builtin_elementwise_fma((f2){n1.x, n1.y}, (f2){iz, iz}, (f2){-oiz, -oiz});
+  const float x0 = txy0.x, y0 = txy0.y, x1 = txy1.x, y1 = txy1.y, z0 = tz.x, z1 = tz.y;
+#else
+  const float x0 = __builtin_fmaf(n0.x, ix, -oix), x1 = __builtin_fmaf(n0.z, ix, -oix);
+  const float y0 = __builtin_fmaf(n0.y, iy, -oiy), y1 = __builtin_fmaf(n0.w, iy, -oiy);
+  const float z0 = __builtin_fmaf(n1.x, iz, -oiz), z1 = __builtin_fmaf(n1.y, iz, -oiz);
+#endif
 #if PSRT_SLAB_ASM
   // v_min3/v_max3 directly: no NaN canonicalisation of tlo / tmax per box
   // (NaN cannot occur: finite boxes, safe_inv directions, finite tmax)
@@ -692,7 +725,7 @@ __device__ __forceinline__ double root_box_entry(const BvhView& bv, double ox, d
   const float4 ra = bv.nodes[0], rb = bv.nodes[1];
   double t0 = 0.0, t1 = tmax;
   const double o3[3] = {ox, oy, oz}, d3[3] = {dx, dy, dz};
-  const double lo3[3] = {ra.x, ra.y, ra.z}, hi3[3] = {rb.x, rb.y, rb.z};
+  const double lo3[3] = {ra.x, ra.y, rb.x}, hi3[3] = {ra.z, ra.w, rb.y};  // DevNode layout
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     if (d3[k] == 0.0) {
@@ -762,25 +795,25 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
       const int leaf_a = __float_as_int(a1.w), leaf_b = __float_as_int(b1.w);
       int next;
       if (!hit_a) {
-        next = __float_as_int(a0.w);
+        next = __float_as_int(a1.z);
       } else if (leaf_a >= 0) {
         leaf = leaf_a;
-        next = __float_as_int(a0.w);
+        next = __float_as_int(a1.z);
       } else if (!slab_hit(b0, b1, ix, iy, iz, oix, oiy, oiz, tlo, tmax)) {
-        next = __float_as_int(b0.w);
+        next = __float_as_int(b1.z);
       } else if (leaf_b >= 0) {
         leaf = leaf_b;
-        next = __float_as_int(b0.w);
+        next = __float_as_int(b1.z);
       } else {
 #if PSRT_TRIP3
         // node+1 is an interior hit too: its first child node+2 in this trip
         const float4 c0 = nodes[2 * node + 4], c1 = nodes[2 * node + 5];
         const int leaf_c = __float_as_int(c1.w);
         if (!slab_hit(c0, c1, ix, iy, iz, oix, oiy, oiz, tlo, tmax)) {
-          next = __float_as_int(c0.w);
+          next = __float_as_int(c1.z);
         } else if (leaf_c >= 0) {
           leaf = leaf_c;
-          next = __float_as_int(c0.w);
+          next = __float_as_int(c1.z);
         } else {
           next = node + 3;
         }
@@ -878,15 +911,18 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   const unsigned lane = lane_id();
   const uint64_t total = a.total_units;
 
-  // BVH nodes staged in LDS when they fit (kLdsNodes x 32 B); the walk's
+  // BVH nodes staged in LDS when they fit (lds_layout; host: lds_max); the walk's
   // dependent node loads then see LDS latency instead of L1/L2 latency
   // With kLds, the spheres (geo, 1/r) are staged as well: the per-lane gathers
   // (previous-hit test, grid cell items, the hit record) then read LDS.
-  __shared__ float4 s_nodes[kLds ? 2 * kLdsNodes : 1];
-  __shared__ double4 s_geo[kLds ? kLdsSpheres : 1];
-  __shared__ double s_inv[kLds ? kLdsSpheres : 1];
-  __shared__ int s_leaf[kLds ? kLdsSpheres : 1];
-  __shared__ int s_nb[kLds ? kLdsSpheres : 1];
+  // (dynamic LDS, sized by the host for this scene: psrt_kernels.h lds_layout)
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+  const LdsLayout lay = lds_layout(a.n, bv.n_nodes, bv.n_leaf);
+  float4* const s_nodes = (float4*)(s_dyn + lay.nodes);
+  double4* const s_geo = (double4*)(s_dyn + lay.geo);
+  double* const s_inv = (double*)(s_dyn + lay.inv);
+  int* const s_leaf = (int*)(s_dyn + lay.leaf);
+  int* const s_nb = (int*)(s_dyn + lay.nb);
   // Constants only the refill block reads (camera basis, image size, the
   // divisions' magic numbers, the seed) live in LDS and are re-read on every
   // refill through an offset the compiler cannot see through: held across
@@ -912,7 +948,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     s_rc.row_stride = a.row_stride;
     s_rc.s_begin = a.s_begin;
   }
-  if constexpr (kLds) {  // host guarantees n_nodes < kLdsNodes and n <= kLdsSpheres
+  if constexpr (kLds) {  // the host sized the dynamic LDS by lds_layout
     for (int e = threadIdx.x; e < 2 * (bv.n_nodes + 1); e += blockDim.x) s_nodes[e] = bv.nodes[e];
     for (int e = threadIdx.x; e < a.n; e += blockDim.x) s_geo[e] = geo[e], s_inv[e] = inv_r[e];
     for (int e = threadIdx.x; e < bv.n_leaf; e += blockDim.x) s_leaf[e] = bv.leaf_idx[e];
