@@ -68,6 +68,45 @@ __device__ __forceinline__ double pm1_of(uint32_t x) {
   return (double)(int)(2u * x - 0x80000000u) * 0x1p-31;
 }
 
+// The raw PCG32 XSH-RR output of state `old` (32 bits); rand() = raw >> 1.
+__device__ __forceinline__ uint32_t pcg_raw32(uint64_t old) {
+  const uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
+  const uint32_t rot = (uint32_t)(old >> 59);
+  return (xs >> rot) | (xs << ((32u - rot) & 31u));
+}
+
+// rand31_x3 without the final >> 1 of each draw (see pm1_raw)
+__device__ __forceinline__ void raw32_x3(uint64_t s0, uint32_t& r0, uint32_t& r1, uint32_t& r2,
+                                         uint64_t& next) {
+  const uint64_t s1 = s0 * 6364136223846793005ULL + 1442695040888963407ULL;
+  const uint64_t s2 = s0 * 0x685f98a2018fade9ULL + 0x1a08ee1184ba6d32ULL;
+  const uint64_t s3 = s0 * 0x0b046976f22528f5ULL + 0x9af678222e728119ULL;
+  r0 = pcg_raw32(s0);
+  r1 = pcg_raw32(s1);
+  r2 = pcg_raw32(s2);
+  next = s3;
+}
+
+// pm1_of(raw >> 1), from the raw 32-bit output: 2 (raw >> 1) = raw & ~1, and
+// subtracting 2^31 mod 2^32 flips the top bit (one v_bitop3_b32).
+__device__ __forceinline__ int pm1_int_raw(uint32_t raw) {
+  return (int)((raw & 0xFFFFFFFEu) ^ 0x80000000u);
+}
+__device__ __forceinline__ double pm1_raw(uint32_t raw) {
+  return (double)pm1_int_raw(raw) * 0x1p-31;
+}
+
+// random_in_unit_sphere's test !((x*x + y*y) + z*z > 1) (vec3.h:88) on
+// x = w_x 2^-31 etc. (w: pm1_int_raw): every product and sum of the
+// reference's expression is the same computation on w scaled by 2^-62 (power
+// of two, no under/overflow: |w| <= 2^31), so rounding commutes with the
+// scale and the test is !((wx*wx + wy*wy) + wz*wz > 2^62) on the doubles w.
+__device__ __forceinline__ bool in_unit_sphere_raw(uint32_t x, uint32_t y, uint32_t z) {
+  const double wx = (double)pm1_int_raw(x), wy = (double)pm1_int_raw(y),
+               wz = (double)pm1_int_raw(z);
+  return !((wx * wx + wy * wy) + wz * wz > 0x1p62);
+}
+
 // random_in_unit_sphere's test (vec3.h:88): !(v.x*v.x + v.y*v.y + v.z*v.z > 1)
 // on v = random(-1, 1) from raw draws (x, y, z), decided exactly in integers.
 // With w = draw - 2^30, each coordinate is w * 2^-30 (pm1_of), so the exact

@@ -868,6 +868,10 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
 #define PSRT_LDS_LEAVES 1  // leaf index + sphere reads from LDS in the walk
 #endif
 
+#ifndef PSRT_RAW_TRIALS
+#define PSRT_RAW_TRIALS 1  // queue raw PCG outputs; the in-sphere test on unscaled doubles
+#endif
+
 #ifndef PSRT_INT_SPHERE
 #define PSRT_INT_SPHERE 0  // random_in_unit_sphere's test in int64 (psrt_device.h); measured slower
 #endif
@@ -1249,7 +1253,11 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
         if (go) clk.util(kUTrial);
         uint32_t z, y, x;
         uint64_t nxt;
+#if PSRT_RAW_TRIALS
+        raw32_x3(rng, z, y, x, nxt);  // z, y, x: g++'s draw order (vec3.h:78-81); raw outputs
+#else
         rand31_x3(rng, z, y, x, nxt);  // z, y, x: g++'s draw order (vec3.h:78-81)
+#endif
 #if PSRT_ABLATE == 2  // measurement only: a second trial computed and sunk
         {
           uint64_t r2 = rng ^ 0x9E3779B97F4A7C15ULL;
@@ -1261,7 +1269,9 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
           ablate_sink += (unsigned)!((c2 * c2 + b2 * b2) + a2 * a2 > 1.0) + (unsigned)n2;
         }
 #endif
-#if PSRT_INT_SPHERE
+#if PSRT_RAW_TRIALS
+        const bool in = in_unit_sphere_raw(x, y, z);
+#elif PSRT_INT_SPHERE
         const bool in = in_unit_sphere(x, y, z);
 #else
         const double rz = pm1_of(z), ry = pm1_of(y), rx = pm1_of(x);
@@ -1292,7 +1302,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
         double x0 = ox;
         asm volatile("" : "+v"(x0));
         const HitRec h2 = hit_record_of(lgeo[hit], linv[hit], t, x0, oy, oz, dx, dy, dz);
-        double sx = pm1_of(q0x), sy = pm1_of(q0y), sz = pm1_of(q0z);
+        double sx = pm1_raw(q0x), sy = pm1_raw(q0y), sz = pm1_raw(q0z);
         if (!((sx * h2.nx + sy * h2.ny) + sz * h2.nz > 0.0)) sx = -sx, sy = -sy, sz = -sz;
         const double ex = ((h2.px + h2.nx) + sx) - h2.px, ey = ((h2.py + h2.ny) + sy) - h2.py,
                      ez = ((h2.pz + h2.nz) + sz) - h2.pz;
@@ -1301,7 +1311,11 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
 #endif
       const HitRec h = hit_record_of(lgeo[hit], linv[hit], t, ox, oy, oz, dx, dy, dz);
       // vec3.h:78-81 random(-1, 1) from the queued draws; vec3.h:102-109 flip
+#if PSRT_RAW_TRIALS
+      double rx = pm1_raw(q0x), ry = pm1_raw(q0y), rz = pm1_raw(q0z);
+#else
       double rx = pm1_of(q0x), ry = pm1_of(q0y), rz = pm1_of(q0z);
+#endif
       q0x = q1x, q0y = q1y, q0z = q1z;
 #if PSRT_QDEPTH > 2
       q1x = q2x, q1y = q2y, q1z = q2z;
