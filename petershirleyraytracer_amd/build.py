@@ -53,8 +53,9 @@ def build_lib(force: bool = False, verbose: bool = False, out: str = LIB,
     srcs = [os.path.join(CSRC, s) for s in LIB_SOURCES]
     if not force and _newer(out, _deps()):
         return out
-    cmd = [HIPCC, f"--offload-arch={ARCH}", *COMMON, *[f"-D{d}" for d in defines], "-fPIC",
-           "-shared", "-o", out, *srcs]
+    extra = os.environ.get("PSRT_HIPCC_FLAGS", "").split()  # tuning builds only
+    cmd = [HIPCC, f"--offload-arch={ARCH}", *COMMON, *extra, *[f"-D{d}" for d in defines],
+           "-fPIC", "-shared", "-o", out, *srcs]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)

@@ -230,7 +230,7 @@ int rt_context_create(int device, rt_context** out) {
     }
   }
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  HIP_TRY(hipMalloc(&c->d_counters, 64 * sizeof(unsigned long long)));
+  HIP_TRY(hipMalloc(&c->d_counters, 128 * sizeof(unsigned long long)));
   HIP_TRY(hipEventCreate(&c->ev_all0));
   HIP_TRY(hipEventCreate(&c->ev_all1));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_plist, hipEventDisableTiming));
@@ -483,7 +483,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   // starts after it (same stream: stream order already does it).
   if (c->in_flight && st != c->last_stream) HIP_TRY(hipStreamWaitEvent(st, c->ev_all1, 0));
   if (P == 0) {  // a shard that owns no rows: zero counters, no launch
-    HIP_TRY(hipMemsetAsync(c->d_counters + 1, 0, 63 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(c->d_counters + 1, 0, 127 * sizeof(unsigned long long), st));
     HIP_TRY(hipEventRecord(c->ev_all0, st));
     HIP_TRY(hipEventRecord(c->ev_all1, st));
     c->in_flight = true;
@@ -537,7 +537,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   ta.work_counter = c->d_counters;
   ta.ray_counter = c->d_counters + 1;
 
-  HIP_TRY(hipMemsetAsync(c->d_counters + 1, 0, 63 * sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(c->d_counters + 1, 0, 127 * sizeof(unsigned long long), st));
   const bool stamps = std::getenv("PSRT_STAMPS") != nullptr;  // diagnostic build
   ta.stamps = c->d_counters + 8;
   ta.wave_log = nullptr;
@@ -725,14 +725,15 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   c->last.kernel_ms = kms;
   c->last.total_ms = all;
   if (std::getenv("PSRT_STAMPS")) {
-    unsigned long long sec[50];
+    unsigned long long sec[60];
     HIP_TRY(hipMemcpy(sec, c->d_counters + 8, sizeof sec, hipMemcpyDeviceToHost));
-    static const char* names[19] = {"refill", "store", "hit", "hint", "nb", "cam",
+    static const char* names[24] = {"refill", "store", "hit", "hint", "nb", "cam",
                                     "grid", "walk", "trial", "scatter", "hint_hit",
                                     "hint_tiny", "grid_cell", "grid_out", "grid_none_fin",
-                                    "grid_none_inf", "far_miss", "park", "list_trip"};
+                                    "grid_none_inf", "far_miss", "park", "list_trip",
+                                    "walk_bvh", "walk_big", "walk_miss", "walk_fin", "walk_inf"};
     std::string u = "{\"psrt_util\": {";
-    for (int k = 0; k < 19; ++k) {
+    for (int k = 0; k < 24; ++k) {
       char b[128];
       const double w = (double)sec[12 + 2 * k], l = (double)sec[13 + 2 * k];
       std::snprintf(b, sizeof b, "%s\"%s\": [%.4g, %.2f]", k ? ", " : "", names[k], w,

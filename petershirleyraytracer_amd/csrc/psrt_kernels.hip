@@ -67,7 +67,10 @@ enum Util { kURefill = 0, kUStore, kUHit, kUHint, kUNb, kUCam, kUGrid, kUWalk, k
             kUScatter,
             // hit_quick outcomes (lanes per wave execution, counted where decided)
             kUHintHit, kUHintTiny, kUGridCell, kUGridOut, kUGridNoneFin, kUGridNoneInf,
-            kUFarMiss, kUPark, kUListTrip, kUCount };
+            kUFarMiss, kUPark, kUListTrip,
+            // walk outcomes: {rays, summed box tests} by result (BVH sphere / big / none)
+            // and by whether the ray parked with a finite bound
+            kUWBvh, kUWBig, kUWMiss, kUWFin, kUWInf, kUCount };
 
 __device__ __forceinline__ bool first_active_lane();
 
@@ -84,6 +87,13 @@ struct SectionClock {
         atomicAdd(ucnt + 2 * u, 1u);
         atomicAdd(ucnt + 2 * u + 1, (unsigned)__popcll(m));
       }
+    }
+  }
+  // diagnostic: per lane, {lanes, sum of v} into probe u (LDS atomics)
+  __device__ __forceinline__ void add(int u, unsigned v) {
+    if constexpr (kOn) {
+      atomicAdd(ucnt + 2 * u, 1u);
+      atomicAdd(ucnt + 2 * u + 1, v);
     }
   }
   __device__ __forceinline__ void start() {
@@ -980,6 +990,8 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   unsigned rays = 0;
   int hint = -1;  // sphere the ray starts on (the previous hit), tested first
   bool pending = false;  // parked for the next batched BVH pass
+  unsigned wbox0 = 0;    // diagnostic build: box tests before this ray's walk
+  bool wfin = false;     // diagnostic build: the parked ray had a finite bound
   int wnode = 0;         // where the parked ray's walk resumes
   bool sc_wait = false;  // hit resolved (pbi, pbt), scatter waits for a queued trial
   // look-ahead of random_in_unit_sphere (vec3.h:83-95): accepted trials, in
@@ -1176,6 +1188,10 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
                                cs, clk, trapped, q, lnb, gc);
           pending = !resolved;
           wnode = 0;
+          if constexpr (kStamps) {
+            wbox0 = cs.boxes;
+            wfin = pbt < 1e30;
+          }
           if (trapped && k < a.max_depth) {
             // the reference traces the max_depth - k rays that remain, all at
             // t = +-0 on this sphere, then returns black (pbi >= 0 below)
@@ -1223,6 +1239,13 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
           if (wnode >= bv.n_nodes) {
             pending = false;
             resolved = true;
+            if constexpr (kStamps) {
+              const unsigned wb = cs.boxes - wbox0;
+              bool big = false;
+              for (int b = 0; b < bv.n_big; ++b) big = big || bv.big_idx[b] == pbi;
+              clk.add(pbi < 0 ? kUWMiss : big ? kUWBig : kUWBvh, wb);
+              clk.add(wfin ? kUWFin : kUWInf, wb);
+            }
           }
         }
       }
