@@ -85,8 +85,6 @@ struct rt_context {
   int grid = 0;       // resident blocks of psrt_trace<false>
   int grid_bvh = 0;   // resident blocks of psrt_trace<true>
   unsigned lds_max = 0;  // largest dynamic LDS that keeps grid_bvh resident (staged scenes)
-  int grid_walk = 0;      // resident blocks of psrt_trace<true, .., kWalker> (walk server)
-  unsigned lds_max_walk = 0;
   // exact-culling structure (psrt_bvh.h)
   bool bvh = false;
   float4* d_nodes = nullptr;
@@ -214,32 +212,23 @@ int rt_context_create(int device, rt_context** out) {
   HIP_TRY(hipGetDeviceProperties(&prop, device));
   c->cus = prop.multiProcessorCount;
   int per_cu = 0;
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &per_cu, psrt::psrt_trace<false, false, false, false>, psrt::kTraceBlock, 0));
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace<false, false, false>,
+                                                        psrt::kTraceBlock, 0));
   c->grid = c->cus * (per_cu < 1 ? 1 : per_cu);
-  // the staged-scene variants keep their residency up to lds_max bytes of
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace<true, false, false>,
+                                                        psrt::kTraceBlock, 0));
+  c->grid_bvh = c->cus * (per_cu < 1 ? 1 : per_cu);
+  // the staged-scene variant keeps that residency up to lds_max bytes of
   // dynamic LDS (largest multiple of 256 B the occupancy query accepts)
-  auto resident = [&](auto plain, auto staged, int* grid, unsigned* lds_max) -> int {
-    int pc0 = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc0, plain, psrt::kTraceBlock, 0));
-    *grid = c->cus * (pc0 < 1 ? 1 : pc0);
-    for (unsigned b = 65536; b >= 256; b -= 256) {
-      int pc = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, staged, psrt::kTraceBlock, b) ==
-              hipSuccess &&
-          pc >= pc0) {
-        *lds_max = b;
-        break;
-      }
+  for (unsigned b = 65536; b >= 256; b -= 256) {
+    int pc = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, psrt::psrt_trace<true, false, true>,
+                                                     psrt::kTraceBlock, b) == hipSuccess &&
+        pc >= per_cu) {
+      c->lds_max = b;
+      break;
     }
-    return RT_OK;
-  };
-  int rc0 = resident(psrt::psrt_trace<true, false, false, false>,
-                     psrt::psrt_trace<true, false, true, false>, &c->grid_bvh, &c->lds_max);
-  if (!rc0)
-    rc0 = resident(psrt::psrt_trace<true, false, false, true>,
-                   psrt::psrt_trace<true, false, true, true>, &c->grid_walk, &c->lds_max_walk);
-  if (rc0) return rc0;
+  }
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIP_TRY(hipMalloc(&c->d_counters, 128 * sizeof(unsigned long long)));
   HIP_TRY(hipEventCreate(&c->ev_all0));
@@ -447,12 +436,12 @@ static int check_params(const rt_params* p) {
 // kLinearChunk units: there the queue's atomics and the per-wave start-up
 // cost more than the launch tail (C1: 0.31 ms with 1024-unit tickets on a few
 // hundred waves vs 0.51 ms guided; C2 -7% guided).
-static void queue_phases(psrt::TraceArgs& ta, int grid, bool guided, int trace_waves) {
+static void queue_phases(psrt::TraceArgs& ta, int grid, bool guided) {
   const char* ek = std::getenv("PSRT_QUEUE_K");
   const char* ed = std::getenv("PSRT_QUEUE_D");
   const double k = ek ? std::atof(ek) : 1.0;
   const double d = ed ? std::atof(ed) : 4.0;  // 8 before frame pipelining (bench.py)
-  const uint64_t waves = (uint64_t)grid * (uint64_t)trace_waves;
+  const uint64_t waves = (uint64_t)grid * (psrt::kTraceBlock / 64);
   unsigned s0 = guided ? psrt::kWorkChunk : psrt::kLinearChunk;
   while (guided && s0 > 64 && (double)ta.total_units < d * (double)waves * (double)s0) s0 >>= 1;
   unsigned size[psrt::kQueuePhases];
@@ -598,17 +587,6 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     }
   }
   const bool use_bvh = c->bvh && !(p->flags & RT_FLAG_NO_CULL);
-  // BVH walks by the workgroup's walk server; PSRT_NO_WALKER:
-  // each wave walks its own parked rays (and the diagnostic build always does)
-  const bool walker = use_bvh && !stamps && !std::getenv("PSRT_NO_WALKER");
-  if (walker) {
-    const char* wt = std::getenv("PSRT_WALKER_TAIL");  // tuning knobs
-    ta.walker_tail = wt ? (unsigned)std::atoi(wt) : 8u;
-    const char* wm = std::getenv("PSRT_WALKER_MIN");
-    ta.walker_min = wm ? (unsigned)std::atoi(wm) : 0u;
-    const char* ww = std::getenv("PSRT_WALK_WAIT");
-    ta.walk_wait = ww ? (unsigned)std::atoi(ww) : 24u;
-  }
   psrt::BvhView bv = bvh_view(c);
   bv.fixpoint = !(p->flags & RT_FLAG_NO_FIXPOINT) && !std::getenv("PSRT_NO_FIXPOINT");
   // camera-ray candidate lists: BVH scenes whose indices fit uint16 and whose
@@ -666,8 +644,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     ta.s_count = sc;
     ta.div_s = fast_div_make((unsigned)sc);
     ta.total_units = (uint64_t)P * sc;
-    queue_phases(ta, walker ? c->grid_walk : use_bvh ? c->grid_bvh : c->grid, use_bvh,
-                 walker ? psrt::kTraceWaves : psrt::kTraceBlock / 64);
+    queue_phases(ta, use_bvh ? c->grid_bvh : c->grid, use_bvh);
     HIP_TRY(hipMemsetAsync(c->d_counters, 0, sizeof(unsigned long long), st));
     HIP_TRY(hipEventRecord(c->ev[2 * ch], st));
     const double4* g4 = c->d_geo;
@@ -676,8 +653,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     // scene data in LDS when three workgroups per CU still fit (the BVH
     // kernel's resident count otherwise: its global-memory variant)
     const unsigned lds_bytes = psrt::lds_layout(c->n, c->n_nodes, c->n_leaf).bytes;
-    const bool lds = use_bvh && lds_bytes <= (walker ? c->lds_max_walk : c->lds_max) &&
-                     !std::getenv("PSRT_NO_LDS");
+    const bool lds = use_bvh && lds_bytes <= c->lds_max && !std::getenv("PSRT_NO_LDS");
     // PSRT_BLOCKS_PER_CU: measurement knob (occupancy sweep), default = resident max
     const char* bpc = std::getenv("PSRT_BLOCKS_PER_CU");
     auto launch = [&](auto kern, int grid) {
@@ -686,17 +662,14 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
                          bv);
     };
     if (!use_bvh)
-      stamps ? launch(psrt::psrt_trace<false, true, false, false>, c->grid)
-             : launch(psrt::psrt_trace<false, false, false, false>, c->grid);
-    else if (walker)
-      lds ? launch(psrt::psrt_trace<true, false, true, true>, c->grid_walk)
-          : launch(psrt::psrt_trace<true, false, false, true>, c->grid_walk);
+      stamps ? launch(psrt::psrt_trace<false, true, false>, c->grid)
+             : launch(psrt::psrt_trace<false, false, false>, c->grid);
     else if (lds)
-      stamps ? launch(psrt::psrt_trace<true, true, true, false>, c->grid_bvh)
-             : launch(psrt::psrt_trace<true, false, true, false>, c->grid_bvh);
+      stamps ? launch(psrt::psrt_trace<true, true, true>, c->grid_bvh)
+             : launch(psrt::psrt_trace<true, false, true>, c->grid_bvh);
     else
-      stamps ? launch(psrt::psrt_trace<true, true, false, false>, c->grid_bvh)
-             : launch(psrt::psrt_trace<true, false, false, false>, c->grid_bvh);
+      stamps ? launch(psrt::psrt_trace<true, true, false>, c->grid_bvh)
+             : launch(psrt::psrt_trace<true, false, false>, c->grid_bvh);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[2 * ch + 1], st));
     psrt::ReduceArgs ra{};
@@ -751,18 +724,6 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   c->last.rays_traced = cnt[3];
   c->last.kernel_ms = kms;
   c->last.total_ms = all;
-  if (std::getenv("PSRT_WALK_DIAG")) {  // diagnostic build (PSRT_WALK_DIAG=1) counters
-    unsigned long long wd[10];
-    HIP_TRY(hipMemcpy(wd, c->d_counters + 100, sizeof wd, hipMemcpyDeviceToHost));
-    std::fprintf(stderr,
-                 "{\"psrt_walk\": {\"rounds\": %llu, \"trips\": %llu, \"lanes_per_trip\": %.2f, "
-                 "\"leaf_passes\": %llu, \"lanes_per_leaf_pass\": %.2f, \"idle\": %llu, "
-                 "\"trace_iters\": %llu, \"trace_stalls\": %llu, \"pending_lanes_per_iter\": %.2f, "
-                 "\"active_lanes_per_iter\": %.2f}}\n",
-                 wd[0], wd[1], wd[1] ? (double)wd[2] / wd[1] : 0.0, wd[3],
-                 wd[3] ? (double)wd[4] / wd[3] : 0.0, wd[5], wd[6], wd[7],
-                 wd[6] ? (double)wd[8] / wd[6] : 0.0, wd[6] ? (double)wd[9] / wd[6] : 0.0);
-  }
   if (std::getenv("PSRT_STAMPS")) {
     unsigned long long sec[60];
     HIP_TRY(hipMemcpy(sec, c->d_counters + 8, sizeof sec, hipMemcpyDeviceToHost));

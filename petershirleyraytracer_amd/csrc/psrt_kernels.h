@@ -81,25 +81,7 @@ struct TraceArgs {
   unsigned walk_tail;               // a BVH pass stops once this few lanes still walk
   FastDiv div_s, div_w;             // unit / s_count, q / width
   unsigned flush_at;                // per-lane counters flush to the totals at this value
-  // BVH walk server (psrt_trace<.., kWalker>): the last waves of each
-  // workgroup walk the rays the other waves park (DESIGN.md §4 "Walk server")
-  unsigned walker_tail;             // a walker round stops its trips once this few lanes walk
-  unsigned walker_min;              // rays the walker gathers before it walks (while waves run)
-  unsigned walk_wait;               // a trace wave iterates once this many lanes can advance
 };
-
-// Waves per workgroup that trace when the walk server runs (the last
-// kWalkers waves walk; trace wave w is served by walker w % kWalkers).
-#ifndef PSRT_WALKERS
-#define PSRT_WALKERS 1
-#endif
-constexpr int kWalkers = PSRT_WALKERS;
-constexpr int kTraceWaves = kTraceBlock / 64 - kWalkers;
-#ifndef PSRT_WALK_SLOTS
-#define PSRT_WALK_SLOTS 16
-#endif
-constexpr int kWalkSlots = PSRT_WALK_SLOTS;  // rays a trace wave can have at the walkers (<= 32)
-static_assert(kWalkSlots >= 1 && kWalkSlots <= 32, "walk slots: a 32-bit free mask");
 
 // BVH node as the device reads it (two float4, from psrt_bvh.h BvhNode):
 // {lo.x, lo.y, hi.x, hi.y}, {lo.z, hi.z, skip, leaf} (skip / leaf: int bits),
@@ -158,7 +140,7 @@ struct ReduceArgs {
   unsigned char* rgb8;    // [pixels][3] or nullptr (last chunk only)
 };
 
-template <bool kBVH, bool kStamps, bool kLds, bool kWalker>
+template <bool kBVH, bool kStamps, bool kLds>
 __global__ void psrt_trace(const double4* __restrict__ geo, const double* __restrict__ inv_r,
                            double* __restrict__ samples, TraceArgs a, BvhView bv);
 __global__ void psrt_reduce(ReduceArgs a);

@@ -917,273 +917,7 @@ __device__ __forceinline__ void flush_counters(const TraceArgs& a, unsigned rays
   }
 }
 
-// ---- BVH walk server (DESIGN.md §4 "Walk server") ---------------------------
-//
-// In a trace wave the parked rays are walked by the lanes that parked them, a
-// few at a time: ~19 of 64 lanes per trip. With kWalker the last kWalkers
-// waves of each workgroup walk instead, for the whole workgroup, and refill a
-// lane as soon as its walk ends, so most trips run with most lanes. The
-// hand-off stays in the workgroup's LDS:
-//   trace wave: each has kWalkSlots ray slots (a wave-uniform free mask). A
-//               parked lane takes a free slot, writes its ray there and puts
-//               the slot id into its walker's ring (one LDS atomicAdd per
-//               wave reserves the ring entries); lanes left without a slot
-//               stay parked and try again next iteration;
-//   walker:     takes slot ids from the ring (single consumer), copies the
-//               rays into its lanes, walks them, writes {bt, bi} back into the
-//               slot, then sets the slot's bit in the trace wave's done mask;
-//   trace wave: every set bit of its done mask is a finished walk of one of
-//               its waiting lanes: those lanes read their results, the wave
-//               clears the bits and frees the slots.
-// One wave's LDS operations execute in order, so a slot's data is in place
-// before the ring entry / done bit that names it. A ring entry reads
-// 0xFFFFFFFF until its producer has written it; the walker stops at the first
-// such entry. The ring holds at most the slots of the waves it serves, so it
-// never wraps onto unread entries. The walk itself is hit_traverse's, ray for
-// ray: the same node sequence and FP64 leaf tests, so the record is the same
-// bits whichever lane walks it.
-#ifndef PSRT_WALKER_PRIO
-#define PSRT_WALKER_PRIO 3  // s_setprio of the walk server's waves (0 = as the trace waves)
-#endif
-#ifndef PSRT_WALK_DIAG
-#define PSRT_WALK_DIAG 0  // diagnostic build: walk-server counters (ray_counter[99..])
-#endif
-// diagnostic counters (first active lane adds; flushed at exit)
-enum WalkDiag { kWdRounds = 0, kWdTrips, kWdLaneTrips, kWdLeafPasses, kWdLaneLeaves, kWdIdle,
-                kWdTraceIters, kWdTraceStall, kWdPendLaneIters, kWdActiveLaneIters, kWdCount };
-
-constexpr int kWalkRingS =  // per walker, >= the slots of the waves it serves (power of two)
-    (kTraceWaves + kWalkers - 1) / kWalkers * kWalkSlots <= 128 ? 128 : 256;
-static_assert((kTraceWaves + kWalkers - 1) / kWalkers * kWalkSlots <= kWalkRingS, "walk ring");
-
-struct WalkShared {
-  double4 rec[kTraceWaves * kWalkSlots][2];  // {o, d.x}, {d.y, d.z, bt, hint << 32 | bi}
-  unsigned ring[kWalkers][kWalkRingS];       // slot ids (wave * kWalkSlots + slot)
-  unsigned long long done[kTraceWaves];      // per trace wave: slots whose walk has finished
-  unsigned tail[kWalkers];                   // ring entries reserved by the trace waves
-  unsigned exited;                           // trace waves that left their loop
-};
-
-// Hand this wave's parked, not yet submitted lanes (`want`) to the walk
-// server, as many as the wave has free slots.
-__device__ __forceinline__ void walk_park(WalkShared& ws, unsigned w, unsigned lane,
-                                          unsigned& slot_free, bool want, bool& sub, int& wslot,
-                                          double ox, double oy, double oz, double dx, double dy,
-                                          double dz, double bt, int bi, int hint) {
-  const uint64_t pm = __ballot(want);
-  if (pm == 0 || slot_free == 0) return;
-  const unsigned n = min((unsigned)__popcll(pm), (unsigned)__popc(slot_free));
-  const unsigned rank = mbcnt64(pm);
-  // rank i takes the i-th free slot
-  unsigned f = slot_free, mine = 0;
-  for (unsigned i = 0; i < n; ++i) {
-    const unsigned sl = (unsigned)__builtin_ctz(f);
-    f &= f - 1u;
-    mine = rank == i ? sl : mine;
-  }
-  slot_free = f;
-  const bool go = want && rank < n;
-  const unsigned id = w * kWalkSlots + mine;
-  if (go) {
-    ws.rec[id][0] = make_double4(ox, oy, oz, dx);
-    ws.rec[id][1] = make_double4(
-        dy, dz, bt, __longlong_as_double((long long)((uint64_t)(unsigned)hint << 32 | (unsigned)bi)));
-    sub = true;
-    wslot = (int)mine;
-  }
-  const unsigned wk = w % kWalkers;
-  const unsigned leader = (unsigned)__builtin_ctzll(pm);
-  unsigned base = 0;
-  if (lane == leader) base = atomicAdd(&ws.tail[wk], n);
-  base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
-  if (go) {
-    volatile unsigned* ring = ws.ring[wk];
-    ring[(base + rank) & (kWalkRingS - 1)] = id;
-  }
-}
-
-// Finished walks of this wave's submitted lanes; true where one arrived (bt, bi set).
-__device__ __forceinline__ bool walk_collect(WalkShared& ws, unsigned w, unsigned lane,
-                                             unsigned& slot_free, bool& sub, int wslot,
-                                             double& bt, int& bi) {
-  const uint64_t dm = __builtin_amdgcn_readfirstlane(
-      __hip_atomic_load(&ws.done[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-  if (dm == 0) return false;
-  // every set bit is the slot of a lane of this wave that waits for it
-  if (lane == 0) atomicAnd(&ws.done[w], ~dm);
-  slot_free |= (unsigned)dm;
-  const bool got = sub && ((dm >> wslot) & 1ull);
-  if (got) {
-    const double4 r = ws.rec[w * kWalkSlots + wslot][1];
-    bt = r.z;
-    bi = (int)(unsigned)__double_as_longlong(r.w);
-    sub = false;
-  }
-  return got;
-}
-
-template <bool kLdsLeaves>
-__device__ __forceinline__ void walk_server(const TraceArgs& a, const BvhView& bv,
-                                         const float4* __restrict__ nodes,
-                                         const int* __restrict__ leaf_idx,
-                                         const double4* __restrict__ lgeo, WalkShared& ws,
-                                         unsigned lane, unsigned wk) {
-  volatile unsigned* ring = ws.ring[wk];
-  unsigned* const tailp = &ws.tail[wk];
-  bool busy = false;
-  unsigned id = 0;
-  double ox = 0, oy = 0, oz = 0, dx = 0, dy = 0, dz = 0, A = 0, bt = 0;
-  int bi = -1, hint = -1, node = bv.n_nodes, leaf = -1;
-  float ix = 0, iy = 0, iz = 0, oix = 0, oiy = 0, oiz = 0, tlo = 0, tmax = 0;
-  double t0w = 0;  // root-box entry of a far origin (hit_traverse's t0)
-  unsigned head = 0;  // wave-uniform: the walker is the ring's only consumer
-  unsigned idle = 0;
-  CullStats cs{0u, 0u};
-  unsigned long long boxes = 0, spheres = 0;
-  unsigned long long wd[kWdCount] = {};
-  if constexpr (PSRT_WALKER_PRIO > 0) __builtin_amdgcn_s_setprio(PSRT_WALKER_PRIO);
-  for (;;) {
-    // ---- refill idle lanes from the ring ----
-    const uint64_t freem = __ballot(!busy);
-    if (freem != 0) {
-      const unsigned tail = __builtin_amdgcn_readfirstlane(
-          __hip_atomic_load(tailp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-      unsigned take = min(tail - head, (unsigned)__popcll(freem));
-      if (take != 0) {
-        const unsigned rank = mbcnt64(freem);
-        const bool cand = !busy && rank < take;
-        unsigned ent = 0xFFFFFFFFu;
-        if (cand) ent = ring[(head + rank) & (kWalkRingS - 1)];
-        const uint64_t bad = __ballot(cand && ent == 0xFFFFFFFFu);
-        if (bad != 0)  // stop at the first slot its producer has not written yet
-          take = (unsigned)__popcll(freem & ((1ull << __builtin_ctzll(bad)) - 1ull));
-        if (!busy && rank < take) {
-          ring[(head + rank) & (kWalkRingS - 1)] = 0xFFFFFFFFu;
-          id = ent;
-          busy = true;
-        }
-        head += take;
-        if (busy && node >= bv.n_nodes) {  // newly taken: copy and set up the ray
-          const double4 r0 = ws.rec[id][0], r1 = ws.rec[id][1];
-          ox = r0.x, oy = r0.y, oz = r0.z, dx = r0.w, dy = r1.x, dz = r1.y, bt = r1.z;
-          const uint64_t hb = (uint64_t)__double_as_longlong(r1.w);
-          bi = (int)(unsigned)hb;
-          hint = (int)(unsigned)(hb >> 32);
-          A = (dx * dx + dy * dy) + dz * dz;  // sphere.cc:9, as the trace lane formed it
-          // hit_traverse's set-up: far origins re-based at their root-box entry
-          double t0 = 0.0;
-          const double am = __builtin_fmax(__builtin_fabs(ox),
-                                           __builtin_fmax(__builtin_fabs(oy), __builtin_fabs(oz)));
-          if (!(am <= bv.r_check))
-            t0 = __builtin_fmax(0.0, root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt));
-          const float fox = (float)(ox + t0 * dx), foy = (float)(oy + t0 * dy),
-                      foz = (float)(oz + t0 * dz);
-          ix = safe_inv((float)dx), iy = safe_inv((float)dy), iz = safe_inv((float)dz);
-          oix = fox * ix, oiy = foy * iy, oiz = foz * iz;
-          tlo = -(float)t0 * 1.00000048f;
-          t0w = t0;
-          tmax = tmax_up(bt - t0);
-          node = 0;
-          leaf = -1;
-        }
-      }
-    }
-    const uint64_t busym = __ballot(busy);
-    if (busym == 0) {
-      if (__hip_atomic_load(&ws.exited, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ==
-          (unsigned)kTraceWaves)
-        break;
-      if (PSRT_WALK_DIAG) ++wd[kWdIdle];
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    // gather a fuller batch while the trace waves still run
-    if ((unsigned)__popcll(busym) < a.walker_min && idle < 4u &&
-        __hip_atomic_load(&ws.exited, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
-      ++idle;
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    idle = 0;
-    // ---- one round: trips until the walking lanes hold leaves (hit_traverse) ----
-    // The last few walking lanes stop early only while the ring holds more
-    // rays (refilled lanes then join them); otherwise they walk on, so every
-    // round makes progress.
-    const bool more = __builtin_amdgcn_readfirstlane(__hip_atomic_load(
-                          tailp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != head;
-    const unsigned cut = more ? a.walker_tail : 0u;
-    if (PSRT_WALK_DIAG) ++wd[kWdRounds];
-    while (node < bv.n_nodes && leaf < 0) {
-      if ((unsigned)__popcll(__ballot(1)) <= cut) break;
-      if (PSRT_WALK_DIAG) {
-        ++wd[kWdTrips];
-        wd[kWdLaneTrips] += (unsigned)__popcll(__ballot(1));
-      }
-      const float4 a0 = nodes[2 * node], a1 = nodes[2 * node + 1];
-      const float4 b0 = nodes[2 * node + 2], b1 = nodes[2 * node + 3];
-      const bool hit_a = slab_hit(a0, a1, ix, iy, iz, oix, oiy, oiz, tlo, tmax);
-      const int leaf_a = __float_as_int(a1.w), leaf_b = __float_as_int(b1.w);
-      int next;
-      if (!hit_a) {
-        next = __float_as_int(a1.z);
-      } else if (leaf_a >= 0) {
-        leaf = leaf_a;
-        next = __float_as_int(a1.z);
-      } else if (!slab_hit(b0, b1, ix, iy, iz, oix, oiy, oiz, tlo, tmax)) {
-        next = __float_as_int(b1.z);
-      } else if (leaf_b >= 0) {
-        leaf = leaf_b;
-        next = __float_as_int(b1.z);
-      } else {
-        next = node + 2;
-      }
-      cs.boxes += 2;
-      node = next;
-    }
-    if (PSRT_WALK_DIAG && __ballot(leaf >= 0) != 0) {
-      ++wd[kWdLeafPasses];
-      wd[kWdLaneLeaves] += (unsigned)__popcll(__ballot(leaf >= 0));
-    }
-    if (leaf >= 0) {
-      const int first = leaf >> 8, cnt = leaf & 255;
-      for (int k = first; k < first + cnt; ++k) {
-        const int idx = leaf_idx[k];
-        if (idx == hint) continue;
-        test_sphere(kLdsLeaves ? lgeo[idx] : bv.leaf_geo[k], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
-        ++cs.spheres;
-      }
-      tmax = tmax_up(bt - t0w);
-      leaf = -1;
-    }
-    // ---- finished walks: result, then the done bit ----
-    const bool fin = busy && node >= bv.n_nodes;
-    if (fin) {  // result into the slot, then the slot's done bit
-      ws.rec[id][1].z = bt;
-      ws.rec[id][1].w = __longlong_as_double((long long)(unsigned)bi);
-      atomicOr(&ws.done[id / kWalkSlots], 1ull << (id % kWalkSlots));
-      busy = false;
-    }
-    // 32-bit lane counters into 64-bit totals before they can wrap
-    if (__builtin_expect(__ballot(max(cs.boxes, cs.spheres) >= 0x40000000u) != 0, 0)) {
-      boxes += cs.boxes, spheres += cs.spheres;
-      cs.boxes = cs.spheres = 0u;
-    }
-  }
-  boxes += cs.boxes, spheres += cs.spheres;
-  for (int off = 32; off > 0; off >>= 1) {
-    boxes += __shfl_xor(boxes, off);
-    spheres += __shfl_xor(spheres, off);
-  }
-  if (lane == 0) {
-    if (spheres) atomicAdd(a.ray_counter + 1, spheres);
-    if (boxes) atomicAdd(a.ray_counter + 2, boxes);
-    if (PSRT_WALK_DIAG)
-      for (int e = 0; e < kWdCount; ++e)
-        if (wd[e]) atomicAdd(a.ray_counter + 99 + e, wd[e]);
-  }
-}
-
-template <bool kBVH, bool kStamps, bool kLds, bool kWalker>
+template <bool kBVH, bool kStamps, bool kLds>
 __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(const double4* __restrict__ geo,
                                                           const double* __restrict__ inv_r,
                                                           double* __restrict__ samples,
@@ -1210,15 +944,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   __shared__ RefillConst s_rc;
   __shared__ GridC s_gc;
   __shared__ unsigned long long s_flush[3];  // counters flushed from the lanes (refill block)
-  __shared__ WalkShared s_walk;              // kWalker only (the walk server's hand-off)
   if (threadIdx.x < 3) s_flush[threadIdx.x] = 0ull;
-  if constexpr (kWalker) {
-    for (int e = threadIdx.x; e < kWalkers * kWalkRingS; e += blockDim.x)
-      (&s_walk.ring[0][0])[e] = 0xFFFFFFFFu;
-    if (threadIdx.x < kTraceWaves) s_walk.done[threadIdx.x] = 0ull;
-    if (threadIdx.x < kWalkers) s_walk.tail[threadIdx.x] = 0u;
-    if (threadIdx.x == 0) s_walk.exited = 0u;
-  }
   if (threadIdx.x == 0) s_gc = grid_consts(bv);
   if (threadIdx.x < 12)
     s_rc.cam[threadIdx.x] = threadIdx.x < 3   ? a.org[threadIdx.x]
@@ -1298,16 +1024,6 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     }
   }
 
-  // kWalker: the last wave serves the workgroup's BVH walks; the others trace
-  const unsigned wv = threadIdx.x / 64;
-  unsigned long long twd[4] = {0, 0, 0, 0};  // PSRT_WALK_DIAG: iterations, stalls, lanes
-  unsigned slot_free = (1u << kWalkSlots) - 1u;  // kWalker: this wave's free walk slots
-  bool wsub = false;                              // kWalker: parked ray handed to the walker
-  int wslot = 0;                                  // kWalker: its slot
-  if (kWalker && wv >= (unsigned)kTraceWaves) {
-    walk_server<kLds && PSRT_LDS_LEAVES>(a, bv, nodes, lleaf, lgeo, s_walk, lane,
-                                         wv - (unsigned)kTraceWaves);
-  } else {
   for (;;) {
     // ---- finish + refill lanes whose sample ended (wavefront ballot compaction) ----
     // The block runs for the wave once at least refill_min lanes are idle (or
@@ -1315,11 +1031,8 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     // for the few iterations they sit idle.
     const bool need = !active;
     const uint64_t need_mask = __ballot(need);
-    // (kWalker: also when every live lane waits for the walk server)
-    const bool run_block =
-        need_mask != 0 && ((unsigned)__popcll(need_mask) >= a.refill_min ||
-                           need_mask == __ballot(1) ||
-                           (kWalker && __ballot(active && !pending) == 0));
+    const bool run_block = need_mask != 0 && ((unsigned)__popcll(need_mask) >= a.refill_min ||
+                                              need_mask == __ballot(1));
     if (run_block) {
       // The per-lane counters are 32-bit. Between two runs of this block a lane
       // adds at most one sample's work (it idles once its sample ends), which the
@@ -1447,36 +1160,8 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     // lanes wait (or nothing else can progress): the pass then runs at high
     // SIMD occupancy instead of once per iteration for a handful of lanes.
     bool resolved = false, finish = false;
-    if constexpr (kWalker && PSRT_WALK_DIAG) {
-      ++twd[0];
-      twd[2] += (unsigned)__popcll(__ballot(pending));
-      twd[3] += (unsigned)__popcll(__ballot(active));
-    }
-    if constexpr (kWalker) {  // walk results the walk server has finished
-      if (__ballot(pending) != 0 && walk_collect(s_walk, wv, lane, slot_free, wsub, wslot, pbt, pbi)) {
-        pending = false;
-        resolved = true;
-      }
-      // An iteration costs the wave the same whatever number of lanes it
-      // advances: while fewer than walk_wait lanes (or half the live ones)
-      // could advance and some wait for walks the walker has, yield the SIMD
-      // (to the walker and the other waves) instead. Lanes still without a
-      // slot wait for the next iteration's walk_park, not for the walker.
-      for (;;) {
-        const unsigned prog = (unsigned)__popcll(__ballot(active && !pending));
-        const unsigned live = (unsigned)__popcll(__ballot(active));
-        if (prog >= min(a.walk_wait, (live + 1) / 2) || __ballot(pending && wsub) == 0) break;
-        if (PSRT_WALK_DIAG) ++twd[1];
-        __builtin_amdgcn_s_sleep(2);
-        if (walk_collect(s_walk, wv, lane, slot_free, wsub, wslot, pbt, pbi)) {
-          pending = false;
-          resolved = true;
-        }
-      }
-    }
-    traced += (unsigned)__popcll(
-        __ballot(active && !pending && !sc_wait && !resolved && a.max_depth >= 0));
-    if (active && !pending && !sc_wait && !resolved) {
+    traced += (unsigned)__popcll(__ballot(active && !pending && !sc_wait && a.max_depth >= 0));
+    if (active && !pending && !sc_wait) {
       if (a.max_depth < 0) {  // main.cc:36-37 at the first call: black, no trace
         finish = true;
       } else {
@@ -1530,11 +1215,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       }
     }
     clk.mark(kSecHit);
-    if constexpr (kWalker) {
-      // hand the newly parked rays to the walk server
-      walk_park(s_walk, wv, lane, slot_free, pending && !wsub, wsub, wslot, ox, oy, oz, dx, dy,
-                dz, pbt, pbi, hint);
-    } else if constexpr (kBVH) {
+    if constexpr (kBVH) {
       const uint64_t pend = __ballot(pending);
       const uint64_t movable = __ballot(active && !pending);
       if (pend != 0 && ((unsigned)__popcll(pend) >= a.batch || movable == 0)) {
@@ -1681,12 +1362,6 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     }
     clk.mark(kSecFillShade);
   }
-  if constexpr (kWalker) {
-    if (lane == 0) atomicAdd(&s_walk.exited, 1u);
-    if (PSRT_WALK_DIAG && lane == 0)
-      for (int e = 0; e < 4; ++e) atomicAdd(a.ray_counter + 99 + kWdTraceIters + e, twd[e]);
-  }
-  }  // trace waves
   if constexpr (kStamps) {
     if (wlog) {
       const unsigned long long t = __builtin_amdgcn_s_memrealtime();
@@ -1711,18 +1386,16 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   if (threadIdx.x < 3 && s_flush[threadIdx.x]) atomicAdd(a.ray_counter + threadIdx.x, s_flush[threadIdx.x]);
 }
 
-#define PSRT_INSTANTIATE(B, S, L, W)                                                       \
-  template __global__ void psrt_trace<B, S, L, W>(const double4* __restrict__,              \
-                                                  const double* __restrict__,              \
-                                                  double* __restrict__, TraceArgs, BvhView);
-PSRT_INSTANTIATE(false, false, false, false)
-PSRT_INSTANTIATE(true, false, false, false)
-PSRT_INSTANTIATE(true, false, true, false)
-PSRT_INSTANTIATE(true, false, false, true)
-PSRT_INSTANTIATE(true, false, true, true)
-PSRT_INSTANTIATE(false, true, false, false)
-PSRT_INSTANTIATE(true, true, false, false)
-PSRT_INSTANTIATE(true, true, true, false)
+#define PSRT_INSTANTIATE(B, S, L)                                                          \
+  template __global__ void psrt_trace<B, S, L>(const double4* __restrict__,                 \
+                                               const double* __restrict__, double* __restrict__, \
+                                               TraceArgs, BvhView);
+PSRT_INSTANTIATE(false, false, false)
+PSRT_INSTANTIATE(true, false, false)
+PSRT_INSTANTIATE(true, false, true)
+PSRT_INSTANTIATE(false, true, false)
+PSRT_INSTANTIATE(true, true, false)
+PSRT_INSTANTIATE(true, true, true)
 #undef PSRT_INSTANTIATE
 
 // pixel_color += sample, in sample order (main.cc:77-84); write_color on the
