@@ -183,7 +183,10 @@ const char* rt_last_error(void) { return g_err.c_str(); }
 int rt_abi_version(void) { return RT_ABI_VERSION; }
 
 const char* rt_build_info(void) {
-  return "psrt gfx950 megakernel (fp64 exact, -ffp-contract=off); trace block " "256";
+#define PSRT_STR2(x) #x
+#define PSRT_STR(x) PSRT_STR2(x)
+  return "psrt gfx950 megakernel (fp64 exact, -ffp-contract=off); trace block " PSRT_STR(
+      PSRT_TRACE_BLOCK) ", work chunk " PSRT_STR(PSRT_WORK_CHUNK);
 }
 
 int rt_device_count(void) {

@@ -114,8 +114,11 @@ static const char* kNames[] = {"v_add_f64",    "v_mul_f64",     "v_fma_f64",    
                                "v_cndmask_b32_e32 vcc", "C select (cmp+cndmask+add+xor)",
                                "v_cmp_gt_u32 -> sgpr"};
 
+static int g_first_op = 0;  // argv[1]: run only the ops from this one on
+
 template <int kOp>
 void run(int cus, double* sink, unsigned long long* dcyc) {
+  if (kOp < g_first_op) return;
   const double n = (double)ITERS * UNROLL * CHAINS;
   double res[2];
   const int waves[3] = {1, 2, 8};
@@ -143,7 +146,7 @@ void run_all(int cus, double* sink, unsigned long long* dcyc) {
   (run<kOps>(cus, sink, dcyc), ...);
 }
 
-int main() {
+int main(int argc, char** argv) {
   int dev = 0;
   hipDeviceProp_t p;
   if (hipGetDeviceProperties(&p, dev) != hipSuccess) {
@@ -157,6 +160,7 @@ int main() {
       hipMalloc(&dcyc, sizeof(unsigned long long)) != hipSuccess)
     return 1;
   run<0>(cus, sink, dcyc);  // warm-up (clocks)
+  if (argc > 1) g_first_op = std::atoi(argv[1]);
   run_all<0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39, 40, 41, 42, 43, 44, 45, 46, 47>(cus, sink, dcyc);
   (void)hipFree(sink);
   (void)hipFree(dcyc);
