@@ -92,8 +92,22 @@ __device__ __forceinline__ void raw32_x3(uint64_t s0, uint32_t& r0, uint32_t& r1
 __device__ __forceinline__ int pm1_int_raw(uint32_t raw) {
   return (int)((raw & 0xFFFFFFFEu) ^ 0x80000000u);
 }
+#ifndef PSRT_CVT_BIAS
+#define PSRT_CVT_BIAS 1  // int -> double through the exponent bias (one FP64 add, no v_cvt)
+#endif
+// (double)pm1_int_raw(raw): with m = raw & ~1, the bits {hi 0x43300000, lo m}
+// are the double 2^52 + m (exact), and (2^52 + m) - (2^52 + 2^31) = m - 2^31
+// is exact (integers below 2^53, the difference below 2^31 in magnitude) and
+// +0 when m = 2^31, as the conversion gives.
+__device__ __forceinline__ double w_raw(uint32_t raw) {
+#if PSRT_CVT_BIAS
+  return __hiloint2double(0x43300000, (int)(raw & 0xFFFFFFFEu)) - 0x1.000008p52;
+#else
+  return (double)pm1_int_raw(raw);
+#endif
+}
 __device__ __forceinline__ double pm1_raw(uint32_t raw) {
-  return (double)pm1_int_raw(raw) * 0x1p-31;
+  return w_raw(raw) * 0x1p-31;
 }
 
 // random_in_unit_sphere's test !((x*x + y*y) + z*z > 1) (vec3.h:88) on
@@ -102,8 +116,7 @@ __device__ __forceinline__ double pm1_raw(uint32_t raw) {
 // of two, no under/overflow: |w| <= 2^31), so rounding commutes with the
 // scale and the test is !((wx*wx + wy*wy) + wz*wz > 2^62) on the doubles w.
 __device__ __forceinline__ bool in_unit_sphere_raw(uint32_t x, uint32_t y, uint32_t z) {
-  const double wx = (double)pm1_int_raw(x), wy = (double)pm1_int_raw(y),
-               wz = (double)pm1_int_raw(z);
+  const double wx = w_raw(x), wy = w_raw(y), wz = w_raw(z);
   return !((wx * wx + wy * wy) + wz * wz > 0x1p62);
 }
 

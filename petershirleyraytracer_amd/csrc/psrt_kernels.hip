@@ -893,6 +893,10 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
 #ifndef PSRT_QDEPTH
 #define PSRT_QDEPTH 2  // look-ahead queue depth (accepted random_in_unit_sphere trials)
 #endif
+#ifndef PSRT_QFLAGS
+#define PSRT_QFLAGS 1  // depth-2 queue occupancy as two lane masks (no integer count)
+#endif
+static_assert(!PSRT_QFLAGS || PSRT_QDEPTH == 2, "queue flags: depth 2 only");
 static_assert(PSRT_QDEPTH == 2 || PSRT_QDEPTH == 3, "queue slots q0..q2 exist");
 
 #ifndef PSRT_TRACE_WAVES
@@ -1001,6 +1005,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   uint32_t q2x = 0, q2y = 0, q2z = 0;
 #endif
   int qn = 0;
+  bool qv0 = false, qv1 = false;  // PSRT_QFLAGS: slot 0 / slot 1 hold a trial
   double pbt = 0.0;      // closest t / index so far of this ray's world.hit
   int pbi = -1;
   CullStats cs{0u, 0u};
@@ -1129,6 +1134,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
           k = 0;
           hint = -1;
           qn = 0;  // the sample's stream starts here: no look-ahead yet
+          qv0 = qv1 = false;
           active = true;
         }
       }
@@ -1272,7 +1278,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       // take it (their stream advances), so the draws stay in stream order
       int f = 0;
       do {
-        const bool go = can_fill && qn < PSRT_QDEPTH;
+        const bool go = can_fill && (PSRT_QFLAGS ? !qv1 : qn < PSRT_QDEPTH);
         if (go) clk.util(kUTrial);
         uint32_t z, y, x;
         uint64_t nxt;
@@ -1302,23 +1308,31 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
 #endif
         rng = go ? nxt : rng;
         const bool push = go && in;
-        const bool to0 = push && qn == 0, to1 = push && qn == 1;
+        const bool to0 = push && (PSRT_QFLAGS ? !qv0 : qn == 0),
+                   to1 = push && (PSRT_QFLAGS ? qv0 : qn == 1);
         q0x = to0 ? x : q0x, q0y = to0 ? y : q0y, q0z = to0 ? z : q0z;
         q1x = to1 ? x : q1x, q1y = to1 ? y : q1y, q1z = to1 ? z : q1z;
 #if PSRT_QDEPTH > 2
         const bool to2 = push && qn == 2;
         q2x = to2 ? x : q2x, q2y = to2 ? y : q2y, q2z = to2 ? z : q2z;
 #endif
-        qn += push ? 1 : 0;
+        if (PSRT_QFLAGS) {
+          qv1 = qv1 || to1;
+          qv0 = qv0 || to0;
+        } else {
+          qn += push ? 1 : 0;
+        }
         ++f;
       } while (f < a.rng_fill ||
-               (f < a.rng_fill + a.rng_extra && __ballot(want && qn == 0) != 0));
+               (f < a.rng_fill + a.rng_extra &&
+                __ballot(want && (PSRT_QFLAGS ? !qv0 : qn == 0)) != 0));
     }
     clk.mark(kSecFillShade);
 
     // ---- scatter: target = (p + n) + random_in_hemisphere(n)  (main.cc:42-43) ----
-    sc_wait = want && qn == 0;
-    if (want && qn > 0) {
+    const bool have = PSRT_QFLAGS ? qv0 : qn > 0;
+    sc_wait = want && !have;
+    if (want && have) {
       clk.util(kUScatter);
 #if PSRT_ABLATE == 9
       {
@@ -1343,7 +1357,12 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
 #if PSRT_QDEPTH > 2
       q1x = q2x, q1y = q2y, q1z = q2z;
 #endif
-      --qn;
+      if (PSRT_QFLAGS) {
+        qv0 = qv1;
+        qv1 = false;
+      } else {
+        --qn;
+      }
       if (!((rx * h.nx + ry * h.ny) + rz * h.nz > 0.0)) rx = -rx, ry = -ry, rz = -rz;
       dx = ((h.px + h.nx) + rx) - h.px;
       dy = ((h.py + h.ny) + ry) - h.py;
