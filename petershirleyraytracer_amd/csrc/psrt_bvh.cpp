@@ -27,8 +27,9 @@ struct Box {
       hi[k] = std::max(hi[k], p[k]);
     }
   }
+  // surface area, the y extent weighted by PSRT_SAH_YW (1 = plain SAH)
   double area() const {
-    const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    const double dx = hi[0] - lo[0], dy = (hi[1] - lo[1]) * PSRT_SAH_YW, dz = hi[2] - lo[2];
     if (!(dx >= 0)) return 0.0;
     return 2.0 * (dx * dy + dy * dz + dz * dx);
   }
@@ -86,41 +87,65 @@ struct Builder {
     return me;
   }
 
-  // binned SAH on the widest centroid axis; -1 = make a leaf
+  // root over prims[b, e) with the fixed children [b, m) and [m, e)
+  int build_split_root(int b, int m, int e) {
+    Box bounds;
+    for (int i = b; i < e; ++i) bounds.grow(prims[i].box);
+    const int me = (int)out.nodes.size();
+    out.nodes.push_back(BvhNode{});
+    for (int k = 0; k < 3; ++k) {
+      out.nodes[me].lo[k] = down(bounds.lo[k]);
+      out.nodes[me].hi[k] = up(bounds.hi[k]);
+    }
+    out.nodes[me].leaf = -1;
+    build(b, m, 1);
+    build(m, e, 1);
+    out.nodes[me].skip = (int32_t)out.nodes.size();
+    return me;
+  }
+
+  // binned SAH (PSRT_SAH_AXES 1: the widest centroid axis; 3: the best of
+  // the three axes); -1 = make a leaf
   int sah_split(int b, int e, const Box& cbox, const Box& bounds) {
-    int axis = 0;
-    double ext = -1;
+    int widest = 0;
+    double wext = -1;
     for (int k = 0; k < 3; ++k)
-      if (cbox.hi[k] - cbox.lo[k] > ext) ext = cbox.hi[k] - cbox.lo[k], axis = k;
+      if (cbox.hi[k] - cbox.lo[k] > wext) wext = cbox.hi[k] - cbox.lo[k], widest = k;
     const int count = e - b;
-    if (!(ext > 0)) {  // coincident centroids: split by count
+    if (!(wext > 0)) {  // coincident centroids: split by count
       return count > 255 ? b + count / 2 : (count > kLeafMax ? b + count / 2 : -1);
     }
     constexpr int kBins = 16;
-    Box bb[kBins];
-    int bc[kBins] = {0};
+    double best = std::numeric_limits<double>::infinity();
+    int best_k = -1, axis = widest;
+    double ext = wext;
+    for (int ax = 0; ax < 3; ++ax) {
+      if (PSRT_SAH_AXES == 1 && ax != widest) continue;
+      const double ex = cbox.hi[ax] - cbox.lo[ax];
+      if (!(ex > 0)) continue;
+      Box bb[kBins];
+      int bc[kBins] = {0};
+      for (int i = b; i < e; ++i) {
+        const int k = std::min(kBins - 1, std::max(0, (int)((prims[i].c[ax] - cbox.lo[ax]) / ex * kBins)));
+        bb[k].grow(prims[i].box);
+        ++bc[k];
+      }
+      for (int k = 1; k < kBins; ++k) {
+        Box l, r;
+        int nl = 0, nr = 0;
+        for (int j = 0; j < k; ++j)
+          if (bc[j]) l.grow(bb[j]), nl += bc[j];
+        for (int j = k; j < kBins; ++j)
+          if (bc[j]) r.grow(bb[j]), nr += bc[j];
+        if (!nl || !nr) continue;
+        const double cost = l.area() * nl + r.area() * nr;
+        if (cost < best) best = cost, best_k = k, axis = ax, ext = ex;
+      }
+    }
     auto bin_of = [&](const Prim& p) {
       int i = (int)((p.c[axis] - cbox.lo[axis]) / ext * kBins);
       return std::min(kBins - 1, std::max(0, i));
     };
-    for (int i = b; i < e; ++i) {
-      const int k = bin_of(prims[i]);
-      bb[k].grow(prims[i].box);
-      ++bc[k];
-    }
-    double best = std::numeric_limits<double>::infinity();
-    int best_k = -1;
-    for (int k = 1; k < kBins; ++k) {
-      Box l, r;
-      int nl = 0, nr = 0;
-      for (int j = 0; j < k; ++j)
-        if (bc[j]) l.grow(bb[j]), nl += bc[j];
-      for (int j = k; j < kBins; ++j)
-        if (bc[j]) r.grow(bb[j]), nr += bc[j];
-      if (!nl || !nr) continue;
-      const double cost = l.area() * nl + r.area() * nr;
-      if (cost < best) best = cost, best_k = k;
-    }
     if (best_k < 0) return b + count / 2;  // all in one bin: split by count
     // cost model: traversal 1, intersection 2 (fp64 test ~ 2 fp32 box tests)
     const double leaf_cost = 2.0 * count;
@@ -183,7 +208,20 @@ BvhHost build_bvh(const rt_sphere* s, int n) {
     prims.push_back(p);
   }
   Builder bld{prims, out};
-  bld.build(0, (int)prims.size(), 0);
+  // Tall spheres (radius > PSRT_TALL_RATIO x median, below the big class: the
+  // final scene's three r = 1 spheres) get a subtree of their own under the
+  // root. Otherwise their tall boxes top every subtree they share, and a
+  // bounce ray leaving the sphere layer upward crosses those boxes for a long
+  // stretch.
+  const double tall = PSRT_TALL_RATIO * median;
+  const auto mid = std::stable_partition(prims.begin(), prims.end(), [&](const Prim& p) {
+    return !(tall > 0 && std::fabs(s[p.idx].r) > tall);
+  });
+  const int m = (int)(mid - prims.begin());
+  if (m > 0 && m < (int)prims.size())
+    bld.build_split_root(0, m, (int)prims.size());
+  else
+    bld.build(0, (int)prims.size(), 0);
   // padding node (never reached: the walk stops at nodes.size()); lets the
   // device read node+1 speculatively. Empty box, leaf word -1, skip = end.
   {

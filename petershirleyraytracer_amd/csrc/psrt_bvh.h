@@ -37,6 +37,15 @@ constexpr double kBigRatio = 16.0;   // radius > 16 x median -> tested every ray
 #ifndef PSRT_LEAF_SAH_MAX
 #define PSRT_LEAF_SAH_MAX 4  // SAH may stop splitting at this many spheres
 #endif
+#ifndef PSRT_SAH_AXES
+#define PSRT_SAH_AXES 3  // binned SAH over the widest centroid axis (1) or all three (3)
+#endif
+#ifndef PSRT_SAH_YW
+#define PSRT_SAH_YW 1.0  // SAH surface areas with the y extent scaled by this
+#endif
+#ifndef PSRT_TALL_RATIO
+#define PSRT_TALL_RATIO 3.0  // > 0: spheres with r > this x median get their own root subtree
+#endif
 #ifndef PSRT_GRID_CELL
 #define PSRT_GRID_CELL 2.5  // grid cell edge in median radii
 #endif
