@@ -93,8 +93,7 @@ def parse():
                     help="trace provably trapped paths to max_depth (DESIGN.md §9)")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="frames in flight (1 = each frame waits for the previous one; "
-                         "0 = auto: 1 for multi-chunk frames, 3 for per-rank frames of "
-                         "<= 32 M samples, else 2)")
+                         "0 = auto: 1 for multi-chunk frames, else 3)")
     ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
                     help="weak: N GPUs render the frame at N x spp (per-GPU work fixed); "
                          "strong: the configured frame on any N")
@@ -254,9 +253,9 @@ def main():
     # auto: overlap only frame tails. Two persistent launches that share the
     # GPU for their whole run are slower than one after the other (C4: -8%).
     # So: 1 in flight when a frame takes several sample chunks (the next
-    # frame would share the GPU with every chunk after the first), 3 for
-    # short per-rank frames (<= 32 M samples: the tail is a large share),
-    # else 2 (a third frame then shares the GPU with the second throughout).
+    # frame would share the GPU with every chunk after the first), else 3
+    # (r02: C3 6970 -> 7016 Msamples/s against 2; a 1/8 shard 2.21 -> 2.13 ms;
+    # C2 within noise).
     per_rank = rows * w * spp
     buf_cap = int(os.environ.get("PSRT_SAMPLE_BUF_MB", "16384")) << 20  # psrt_capi.hip
     if args.pipeline > 0:
@@ -264,7 +263,7 @@ def main():
     elif per_rank * SAMPLE_RECORD_BYTES > buf_cap:
         depth = 1
     else:
-        depth = 3 if per_rank <= 32_000_000 else 2
+        depth = 3
     ctxs = []
     for _ in range(depth):
         c = P.Context(local)
