@@ -45,8 +45,16 @@
 #define PSRT_SLAB_ASM 1  // slab test min/max as inline asm (no per-box NaN canonicalisation)
 #endif
 
+#ifndef PSRT_WALK_PRIO
+#define PSRT_WALK_PRIO 3  // s_setprio of a wave during its batched BVH walk (0 = unchanged)
+#endif
+
+#ifndef PSRT_HIT_PRIO
+#define PSRT_HIT_PRIO 2  // s_setprio of a wave during hit_quick (0 = unchanged)
+#endif
+
 #ifndef PSRT_TAIL_PRIO
-#define PSRT_TAIL_PRIO 0  // s_setprio of a wave once the work queue is empty (0 = unchanged)
+#define PSRT_TAIL_PRIO 1  // s_setprio of a wave once the work queue is empty (0 = unchanged)
 #endif
 
 namespace psrt {
@@ -1167,6 +1175,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     // SIMD occupancy instead of once per iteration for a handful of lanes.
     bool resolved = false, finish = false;
     traced += (unsigned)__popcll(__ballot(active && !pending && !sc_wait && a.max_depth >= 0));
+    if constexpr (PSRT_HIT_PRIO > 0) __builtin_amdgcn_s_setprio(PSRT_HIT_PRIO);
     if (active && !pending && !sc_wait) {
       if (a.max_depth < 0) {  // main.cc:36-37 at the first call: black, no trace
         finish = true;
@@ -1220,11 +1229,16 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
         }
       }
     }
+    if constexpr (PSRT_HIT_PRIO > 0) {  // back to the base priority
+      if (PSRT_TAIL_PRIO > 0 && exhausted) __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
+      else __builtin_amdgcn_s_setprio(0);
+    }
     clk.mark(kSecHit);
     if constexpr (kBVH) {
       const uint64_t pend = __ballot(pending);
       const uint64_t movable = __ballot(active && !pending);
       if (pend != 0 && ((unsigned)__popcll(pend) >= a.batch || movable == 0)) {
+        if constexpr (PSRT_WALK_PRIO > 0) __builtin_amdgcn_s_setprio(PSRT_WALK_PRIO);
         if (pending) {
           clk.util(kUWalk);
 #if PSRT_ABLATE == 3  // measurement only: the walk runs twice, the copy's result sunk
@@ -1253,6 +1267,10 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
               clk.add(wfin ? kUWFin : kUWInf, wb);
             }
           }
+        }
+        if constexpr (PSRT_WALK_PRIO > 0) {
+          if (PSRT_TAIL_PRIO > 0 && exhausted) __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
+          else __builtin_amdgcn_s_setprio(0);
         }
       }
     }
@@ -1419,7 +1437,12 @@ PSRT_INSTANTIATE(true, true, true)
 
 // pixel_color += sample, in sample order (main.cc:77-84); write_color on the
 // last chunk (color.h:8-24).
+#ifndef PSRT_REDUCE_PRIO
+#define PSRT_REDUCE_PRIO 3  // s_setprio of psrt_reduce's waves (they share CUs with the next frame's trace)
+#endif
+
 __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
+  if constexpr (PSRT_REDUCE_PRIO > 0) __builtin_amdgcn_s_setprio(PSRT_REDUCE_PRIO);
   // One wave per 64 pixels. A pixel's samples are contiguous, so the wave
   // stages [64 pixels][kReduceTile samples] tiles through LDS, then each lane
   // adds its pixel's samples in order.
