@@ -49,6 +49,10 @@
 #define PSRT_WALK_PRIO 3  // s_setprio of a wave during its batched BVH walk (0 = unchanged)
 #endif
 
+#ifndef PSRT_NT_STORE
+#define PSRT_NT_STORE 0  // sample records with non-temporal stores
+#endif
+
 #ifndef PSRT_HIT_PRIO
 #define PSRT_HIT_PRIO 2  // s_setprio of a wave during hit_quick (0 = unchanged)
 #endif
@@ -1071,8 +1075,13 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
           kk = (unsigned short)(k < kSampleKCap ? k : kSampleKCap);
         }
         const unsigned u = su;  // < total < 2^32
+#if PSRT_NT_STORE
+        __builtin_nontemporal_store(tt, samples + u);
+        __builtin_nontemporal_store(kk, (unsigned short*)(samples + total) + u);
+#else
         samples[u] = tt;
         ((unsigned short*)(samples + total))[u] = kk;  // k array follows the t array
+#endif
         done = false;
       }
     }
