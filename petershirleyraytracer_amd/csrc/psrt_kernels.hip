@@ -1447,7 +1447,7 @@ PSRT_INSTANTIATE(true, true, true)
 // pixel_color += sample, in sample order (main.cc:77-84); write_color on the
 // last chunk (color.h:8-24).
 #ifndef PSRT_REDUCE_PRIO
-#define PSRT_REDUCE_PRIO 3  // s_setprio of psrt_reduce's waves (they share CUs with the next frame's trace)
+#define PSRT_REDUCE_PRIO 0  // s_setprio of psrt_reduce's waves (they share CUs with the next frame's trace)
 #endif
 
 __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
