@@ -57,6 +57,14 @@
 #define PSRT_HIT_PRIO 2  // s_setprio of a wave during hit_quick (0 = unchanged)
 #endif
 
+#ifndef PSRT_REFILL_PRIO
+#define PSRT_REFILL_PRIO 0  // s_setprio of a wave in its refill block (0 = base)
+#endif
+
+#ifndef PSRT_SCATTER_PRIO
+#define PSRT_SCATTER_PRIO 0  // s_setprio of a wave in its scatter block (0 = base)
+#endif
+
 #ifndef PSRT_TAIL_PRIO
 #define PSRT_TAIL_PRIO 1  // s_setprio of a wave once the work queue is empty (0 = unchanged)
 #endif
@@ -1085,6 +1093,9 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
         done = false;
       }
     }
+    if constexpr (PSRT_REFILL_PRIO > 0) {
+      if (run_block && !exhausted) __builtin_amdgcn_s_setprio(PSRT_REFILL_PRIO);
+    }
     if (run_block && !exhausted) {
       const unsigned cnt = (unsigned)__popcll(need_mask);
       const unsigned rank = mbcnt64(need_mask);
@@ -1172,6 +1183,10 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
           if (wlog && lane == 0) wlog[1] = t, wlog[3] = iters;
         }
       }
+    }
+    if constexpr (PSRT_REFILL_PRIO > 0) {
+      if (PSRT_TAIL_PRIO > 0 && exhausted) __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
+      else __builtin_amdgcn_s_setprio(0);
     }
     clk.mark(kSecRefill);
     if (__ballot(active) == 0) break;
@@ -1359,6 +1374,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     // ---- scatter: target = (p + n) + random_in_hemisphere(n)  (main.cc:42-43) ----
     const bool have = PSRT_QFLAGS ? qv0 : qn > 0;
     sc_wait = want && !have;
+    if constexpr (PSRT_SCATTER_PRIO > 0) __builtin_amdgcn_s_setprio(PSRT_SCATTER_PRIO);
     if (want && have) {
       clk.util(kUScatter);
 #if PSRT_ABLATE == 9
@@ -1398,6 +1414,10 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       A = (dx * dx + dy * dy) + dz * dz;
       hint = hit;
       ++k;
+    }
+    if constexpr (PSRT_SCATTER_PRIO > 0) {
+      if (PSRT_TAIL_PRIO > 0 && exhausted) __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
+      else __builtin_amdgcn_s_setprio(0);
     }
     clk.mark(kSecScatter);
 
