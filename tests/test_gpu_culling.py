@@ -87,6 +87,9 @@ def test_bvh_ties_and_degenerate_scenes():
         "nested": np.concatenate([base, base * [1, 1, 1, 0.5], base * [1, 1, 1, 0.25]]),
         "mixed_big": np.concatenate([base, [[0, -1000, 0, 1000], [0, 0, 0, 40.0],
                                             [5, 5, 5, 1e-9]]]),
+        # tall spheres (3-16x the median radius): the BVH's own root subtree
+        "tall": np.concatenate([base, np.concatenate([rng.uniform(-3, 3, (12, 3)),
+                                                      rng.uniform(1.2, 4.0, (12, 1))], 1)]),
         "negative_r": base * [1, 1, 1, -1],
         "coincident": np.tile([[0.0, 0.0, 0.0, 1.0]], (40, 1)),
     }
@@ -176,6 +179,8 @@ def test_hinted_bounce_rays_contact_scenes():
         "nested": np.concatenate([base, base * [1, 1, 1, 0.5], base * [1, 1, 1, 0.25]]),
         "mixed_big": np.concatenate([base, [[0, -1000, 0, 1000], [0, 0, 0, 40.0],
                                             [5, 5, 5, 1e-9]]]),
+        "tall": np.concatenate([base, np.concatenate([rng.uniform(-3, 3, (12, 3)),
+                                                      rng.uniform(1.2, 4.0, (12, 1))], 1)]),
         "negative_r": base * [1, 1, 1, -1],
         "sparse": np.concatenate([rng.uniform(-40, 40, (60, 3)), rng.uniform(0.2, 1.0, (60, 1))], 1),
     }
