@@ -50,7 +50,7 @@
 #endif
 
 #ifndef PSRT_NT_STORE
-#define PSRT_NT_STORE 0  // sample records with non-temporal stores
+#define PSRT_NT_STORE 1  // sample records with non-temporal stores
 #endif
 
 #ifndef PSRT_HIT_PRIO
