@@ -154,6 +154,22 @@ def test_sampled_pixels_c3_c4(final_scene):
                 assert np.array_equal(bits(acc[0, p["i"]]), bits(unhex(p["accum"]))), p
 
 
+def test_sampled_pixels_c5_multi_chunk(final_scene, monkeypatch):
+    """C5 (1200x800 at 10000 spp): the rows of 8 pixels the reference
+    rendered at full spp (tests/golden/make_c5.py), on a 32 MB sample buffer
+    so that each row takes 4 sample chunks whose running sums continue across
+    launches."""
+    fx = golden("c5_pixels.json")
+    w, h, spp = fx["width"], fx["height"], fx["spp"]
+    cam = np.array(unhex(fx["camera"]))
+    monkeypatch.setenv("PSRT_SAMPLE_BUF_MB", "32")  # 1200 px x 10 B: 2796-sample chunks
+    for p in fx["pixels"]:
+        acc, _, st = P.render(final_scene, cam, w, h, spp, fx["max_depth"], fx["seed"],
+                              row_offset=p["row"], row_stride=h)
+        assert acc.shape == (1, w, 3)
+        assert np.array_equal(bits(acc[0, p["i"]]), bits(unhex(p["accum"]))), p
+
+
 def test_full_frames_match_reference_checksums(final_scene):
     """Full-size frames (C2 two-sphere and C3 final, 1200x800x100) against
     the reference's own full-frame checksums (tests/golden/large.json)."""
