@@ -69,6 +69,11 @@ psrt::FastDiv fast_div_make(unsigned d) {
   return f;
 }
 
+// d_counters layout (words)
+constexpr size_t kHeads = 128;
+constexpr size_t kSets = kHeads + (size_t)psrt::kQueues * psrt::kShardStride;
+constexpr size_t kCounterWords = kSets + (size_t)psrt::kQueues * psrt::kShardStride;
+
 size_t sample_buffer_cap_bytes() {
   const char* e = std::getenv("PSRT_SAMPLE_BUF_MB");
   // default 16 GiB: C4 (41 GB of sample records) in 3 chunks, C5 in 6
@@ -119,7 +124,9 @@ struct rt_context {
   hipEvent_t ev_plist = nullptr;  // after the lists' build (other streams wait on it)
   unsigned long long* d_wave_log = nullptr;  // diagnostic (PSRT_STAMPS): per-wave timeline
   size_t wave_log_cap = 0, wave_log_used = 0;
-  unsigned long long* d_counters = nullptr;  // [0] queue head, [1] rays, [2] tests, [3] boxes
+  // [8, 128) diagnostic stamps; queue heads at kHeads, statistics counter sets
+  // (rays, sphere tests, box tests, traced rays) at kSets, kShardStride apart
+  unsigned long long* d_counters = nullptr;
   std::vector<hipEvent_t> ev;  // pairs around each trace launch
   int ev_used = 0;
   hipEvent_t ev_all0 = nullptr, ev_all1 = nullptr;
@@ -233,7 +240,7 @@ int rt_context_create(int device, rt_context** out) {
     }
   }
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  HIP_TRY(hipMalloc(&c->d_counters, 128 * sizeof(unsigned long long)));
+  HIP_TRY(hipMalloc(&c->d_counters, kCounterWords * sizeof(unsigned long long)));
   HIP_TRY(hipEventCreate(&c->ev_all0));
   HIP_TRY(hipEventCreate(&c->ev_all1));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_plist, hipEventDisableTiming));
@@ -446,6 +453,8 @@ static void queue_phases(psrt::TraceArgs& ta, int grid, bool guided) {
   const double d = ed ? std::atof(ed) : 4.0;  // 8 before frame pipelining (bench.py)
   const uint64_t waves = (uint64_t)grid * (psrt::kTraceBlock / 64);
   unsigned s0 = guided ? psrt::kWorkChunk : psrt::kLinearChunk;
+  if (const char* el = std::getenv("PSRT_LINEAR_CHUNK"); el && !guided)  // tuning knob
+    s0 = std::max(64u, std::min(4096u, (unsigned)std::atoi(el)));
   while (guided && s0 > 64 && (double)ta.total_units < d * (double)waves * (double)s0) s0 >>= 1;
   unsigned size[psrt::kQueuePhases];
   for (int p = 0; p < psrt::kQueuePhases; ++p) size[p] = guided ? std::max(64u, s0 >> p) : s0;
@@ -486,7 +495,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   // starts after it (same stream: stream order already does it).
   if (c->in_flight && st != c->last_stream) HIP_TRY(hipStreamWaitEvent(st, c->ev_all1, 0));
   if (P == 0) {  // a shard that owns no rows: zero counters, no launch
-    HIP_TRY(hipMemsetAsync(c->d_counters + 1, 0, 127 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(c->d_counters, 0, kCounterWords * sizeof(unsigned long long), st));
     HIP_TRY(hipEventRecord(c->ev_all0, st));
     HIP_TRY(hipEventRecord(c->ev_all1, st));
     c->in_flight = true;
@@ -537,10 +546,10 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   ta.pixels = (unsigned)P;
   ta.seedmix = splitmix64_host(p->seed);
   ta.div_w = fast_div_make((unsigned)p->width);
-  ta.work_counter = c->d_counters;
-  ta.ray_counter = c->d_counters + 1;
+  ta.work_counter = c->d_counters + kHeads;
+  ta.ray_counter = c->d_counters + kSets;
 
-  HIP_TRY(hipMemsetAsync(c->d_counters + 1, 0, 127 * sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(c->d_counters, 0, kCounterWords * sizeof(unsigned long long), st));
   const bool stamps = std::getenv("PSRT_STAMPS") != nullptr;  // diagnostic build
   ta.stamps = c->d_counters + 8;
   ta.wave_log = nullptr;
@@ -648,7 +657,9 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     ta.div_s = fast_div_make((unsigned)sc);
     ta.total_units = (uint64_t)P * sc;
     queue_phases(ta, use_bvh ? c->grid_bvh : c->grid, use_bvh);
-    HIP_TRY(hipMemsetAsync(c->d_counters, 0, sizeof(unsigned long long), st));
+    if (ch > 0)  // the heads of the previous chunk's queue
+      HIP_TRY(hipMemsetAsync(c->d_counters + kHeads, 0,
+                             psrt::kQueues * psrt::kShardStride * sizeof(unsigned long long), st));
     HIP_TRY(hipEventRecord(c->ev[2 * ch], st));
     const double4* g4 = c->d_geo;
     const double* ir = c->d_inv_r;
@@ -705,12 +716,15 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   if (!c->in_flight) return set_error(RT_E_INVALID, "rt_context_sync_stats: no render enqueued");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipEventSynchronize(c->ev_all1));
-  unsigned long long cnt[4] = {0, 0, 0, 0};
+  unsigned long long sets[psrt::kQueues * psrt::kShardStride];
   // on the render's own stream: a null-stream copy would also wait for work
   // other contexts queued on other streams (a pipelined next frame)
-  HIP_TRY(hipMemcpyAsync(cnt, c->d_counters + 1, sizeof cnt, hipMemcpyDeviceToHost,
+  HIP_TRY(hipMemcpyAsync(sets, c->d_counters + kSets, sizeof sets, hipMemcpyDeviceToHost,
                          c->last_stream));
   HIP_TRY(hipStreamSynchronize(c->last_stream));
+  unsigned long long cnt[4] = {0, 0, 0, 0};
+  for (int q = 0; q < psrt::kQueues; ++q)
+    for (int k = 0; k < 4; ++k) cnt[k] += sets[psrt::kShardStride * q + k];
   const unsigned long long rays = cnt[0];
   double kms = 0.0;
   for (int ch = 0; ch < c->ev_used; ++ch) {

@@ -16,6 +16,18 @@ constexpr int kTraceBlock = PSRT_TRACE_BLOCK;
 constexpr unsigned kWorkChunk = PSRT_WORK_CHUNK;  // largest queue ticket (units); see queue_phases
 constexpr unsigned kLinearChunk = 1024;           // queue ticket of the small-scene (linear) path
 constexpr int kQueuePhases = 5;        // guided: ticket sizes halve toward the end, >= 64
+#ifndef PSRT_QUEUES
+#define PSRT_QUEUES 8
+#endif
+// Queue heads and statistics counters are sharded: blocks b and b + 8 share an
+// XCD (round-robin placement), and blocks with label b % kQueues share one
+// head / counter set on its own 128-B line. One device-scope head saturates
+// near 88 dequeues/us (MI355X_MICROARCH.md, "dequeue"); small tickets (C1,
+// small shards) ran into that. Global ticket g = t * kQueues + label, where t
+// counts the tickets taken from the label's head; a wave whose head runs past
+// the end of the work moves on to the next heads (stealing) before it stops.
+constexpr int kQueues = PSRT_QUEUES;
+constexpr int kShardStride = 16;       // u64 words between heads / counter sets (128 B)
 // Scene data psrt_trace stages in (dynamic) LDS per workgroup: BVH nodes (2
 // float4 each, plus the padding node), spheres {c, r*r}, 1/r, leaf slots and
 // neighbour words; byte offsets, 16-B aligned. The host stages them when as
@@ -61,7 +73,7 @@ struct TraceArgs {
   int s_begin, s_count; // sample chunk [s_begin, s_begin + s_count)
   uint64_t total_units; // pixels * s_count  (< 2^32)
   uint64_t seedmix;     // splitmix64(seed)
-  unsigned long long* work_counter;  // queue tickets taken (one atomicAdd of 1 per ticket)
+  unsigned long long* work_counter;  // kQueues heads, kShardStride apart (one atomicAdd per ticket)
   // Guided work queue: tickets [ph_first[p], ph_first[p+1]) of phase p cover
   // ph_size[p] units each from unit ph_base[p] on; the last phase is open.
   // Sizes shrink toward the end of the queue, so the last windows are small
@@ -69,7 +81,8 @@ struct TraceArgs {
   uint64_t ph_first[kQueuePhases + 1];
   uint64_t ph_base[kQueuePhases];
   unsigned ph_size[kQueuePhases];
-  unsigned long long* ray_counter;  // [0] rays, [1] sphere tests, [2] box tests
+  unsigned long long* ray_counter;  // kQueues sets, kShardStride apart: [0] rays, [1] sphere
+                                    // tests, [2] box tests, [3] traced rays (host sums them)
   unsigned long long* stamps;       // diagnostic build: cycles per section (kSecCount)
   unsigned long long* wave_log;     // diagnostic build: per wave {start, queue empty, exit,
                                     // iterations at queue empty, at exit} (s_memrealtime,

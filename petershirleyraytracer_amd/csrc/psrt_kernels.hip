@@ -926,8 +926,8 @@ static_assert(PSRT_QDEPTH == 2 || PSRT_QDEPTH == 3, "queue slots q0..q2 exist");
 
 // rays / sphere tests / box tests of this wave (32-bit per lane) -> one 64-bit
 // atomic each. Called converged (whole wave).
-__device__ __forceinline__ void flush_counters(const TraceArgs& a, unsigned rays, unsigned spheres,
-                                            unsigned boxes, unsigned lane) {
+__device__ __forceinline__ void flush_counters(unsigned long long* ctr, unsigned rays,
+                                            unsigned spheres, unsigned boxes, unsigned lane) {
   unsigned long long wr = rays, ws = spheres, wb = boxes;
   for (int off = 32; off > 0; off >>= 1) {
     wr += __shfl_xor(wr, off);
@@ -935,9 +935,9 @@ __device__ __forceinline__ void flush_counters(const TraceArgs& a, unsigned rays
     wb += __shfl_xor(wb, off);
   }
   if (lane == 0) {
-    if (wr) atomicAdd(a.ray_counter, wr);
-    if (ws) atomicAdd(a.ray_counter + 1, ws);
-    if (wb) atomicAdd(a.ray_counter + 2, wb);
+    if (wr) atomicAdd(ctr, wr);
+    if (ws) atomicAdd(ctr + 1, ws);
+    if (wb) atomicAdd(ctr + 2, wb);
   }
 }
 
@@ -1106,13 +1106,19 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       uint64_t nb = 0;
       unsigned wsize = kWorkChunk;
       if (cnt > win_left) {
-        uint64_t tk = 0;
-        if (lane == 0) tk = atomicAdd(a.work_counter, 1ull);
-        tk = __shfl(tk, 0);
-        int ph = 0;
-        while (ph < kQueuePhases - 1 && tk >= a.ph_first[ph + 1]) ++ph;
-        nb = a.ph_base[ph] + (tk - a.ph_first[ph]) * a.ph_size[ph];
-        wsize = a.ph_size[ph];
+        // sharded heads (psrt_kernels.h kQueues): this block's own head first,
+        // then the next ones once it has run past the end of the work
+        for (unsigned qnext = 0;; ++qnext) {
+          const unsigned h = (blockIdx.x + qnext) % kQueues;
+          uint64_t tk = 0;
+          if (lane == 0) tk = atomicAdd(a.work_counter + kShardStride * h, 1ull);
+          tk = __shfl(tk, 0) * kQueues + h;  // global ticket
+          int ph = 0;
+          while (ph < kQueuePhases - 1 && tk >= a.ph_first[ph + 1]) ++ph;
+          nb = a.ph_base[ph] + (tk - a.ph_first[ph]) * a.ph_size[ph];
+          wsize = a.ph_size[ph];
+          if (nb < total || qnext == kQueues - 1) break;
+        }
       }
       if (need) {
         clk.util(kURefill);
@@ -1446,10 +1452,11 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   }
 
   if (PSRT_ABLATE && ablate_sink == 0x9E3779B9u && a.width < 0) samples[0] = ablate_sink;
-  flush_counters(a, rays, cs.spheres, cs.boxes, lane);
-  if (lane == 0 && traced) atomicAdd(a.ray_counter + 3, traced);
+  unsigned long long* const ctr = a.ray_counter + kShardStride * (blockIdx.x % kQueues);
+  flush_counters(ctr, rays, cs.spheres, cs.boxes, lane);
+  if (lane == 0 && traced) atomicAdd(ctr + 3, traced);
   __syncthreads();  // every wave of the block has left the loop (and flushed to LDS)
-  if (threadIdx.x < 3 && s_flush[threadIdx.x]) atomicAdd(a.ray_counter + threadIdx.x, s_flush[threadIdx.x]);
+  if (threadIdx.x < 3 && s_flush[threadIdx.x]) atomicAdd(ctr + threadIdx.x, s_flush[threadIdx.x]);
 }
 
 #define PSRT_INSTANTIATE(B, S, L)                                                          \

@@ -12,7 +12,7 @@ for r in $(seq 1 ${ROUNDS:-2}); do
   for v in ${LIBS:-cur}; do
     L=petershirleyraytracer_amd/lib/libpsrt_$v.so; [ "$v" = cur ] && L=petershirleyraytracer_amd/lib/libpsrt.so
     PSRT_LIB=$L timeout -k 10 120 python bench.py --config $CFG --no-cpu-baseline --steps ${STEPS:-10} --warmup 2 ${BENCH_ARGS} > gpurun_out/var/b_${v}_$r.log 2>&1 || { echo "bench $v failed"; tail -5 gpurun_out/var/b_${v}_$r.log; exit 1; }
-    python3 -c "import json; d=json.loads(open('gpurun_out/var/b_${v}_$r.log').read().strip().splitlines()[-1]); print('$v round $r', 'ms/step', d['ms_per_step'], 'kernel ms', d['roofline']['avg_launch_ms'], 'Msamples/s', d['value'])"
+    python3 -c "import json; d=json.loads(open('gpurun_out/var/b_${v}_$r.log').read().strip().splitlines()[-1]); print('$v round $r', 'ms/step', d['ms_per_step'], 'unpiped', d.get('unpipelined',{}).get('ms_per_step'), 'kernel ms', d['roofline']['avg_launch_ms'], 'Msamples/s', d['value'])"
   done
 done
 if [ -n "$PMC" ]; then
