@@ -213,7 +213,8 @@ def main():
 
     import petershirleyraytracer_amd as P
     from petershirleyraytracer_amd.dist import gather_frame, rows_owned, shard
-    from petershirleyraytracer_amd.render import FLAG_NO_CULL, FLAG_NO_FIXPOINT
+    from petershirleyraytracer_amd.render import (FLAG_NO_CULL, FLAG_NO_FIXPOINT,
+                                                  FLAG_NO_TAIL_PRIORITY)
 
     if os.environ.get("PSRT_BENCH_BACKEND", "nccl") != "nccl":
         local = 0  # rehearsal: every rank on the one GPU
@@ -247,23 +248,27 @@ def main():
     else:
         off, stride = shard(rank, world)
         rows = rows_owned(h, rank, world)
-    prm = P.params(w, h, spp, args.max_depth, args.seed, off, stride,
-                   (FLAG_NO_CULL if args.no_cull else 0)
-                   | (FLAG_NO_FIXPOINT if args.no_fixpoint else 0))
-    # auto: overlap only frame tails. Two persistent launches that share the
-    # GPU for their whole run are slower than one after the other (C4: -8%).
-    # So: 1 in flight when a frame takes several sample chunks (the next
-    # frame would share the GPU with every chunk after the first), else 3
-    # (r02: C3 6970 -> 7016 Msamples/s against 2; a 1/8 shard 2.21 -> 2.13 ms;
-    # C2 within noise).
+    flags = ((FLAG_NO_CULL if args.no_cull else 0)
+             | (FLAG_NO_FIXPOINT if args.no_fixpoint else 0))
+    prm = P.params(w, h, spp, args.max_depth, args.seed, off, stride, flags)
+    prm_notail = P.params(w, h, spp, args.max_depth, args.seed, off, stride,
+                          flags | FLAG_NO_TAIL_PRIORITY)
+    # Frames in flight. Two persistent launches that share the GPU for their
+    # whole run are slower than one after the other (C4: -8%), so a frame of
+    # several sample chunks runs alone (depth 1). Otherwise the depth is
+    # picked by measurement on this GPU (`tuning` below, untimed runs).
     per_rank = rows * w * spp
     buf_cap = int(os.environ.get("PSRT_SAMPLE_BUF_MB", "16384")) << 20  # psrt_capi.hip
+    # candidates: (frames in flight, tail priority, gated): gated = a frame's
+    # trace waits on the device for frame - 2 to finish, so that at most two
+    # traces are in flight and the next one fills only the running one's tail
     if args.pipeline > 0:
-        depth = args.pipeline
+        candidates = [(args.pipeline, True, False)]
     elif per_rank * SAMPLE_RECORD_BYTES > buf_cap:
-        depth = 1
+        candidates = [(1, True, False)]
     else:
-        depth = 3
+        candidates = [(1, True, False), (2, True, False), (3, True, False), (3, True, True)]
+    depth = max(c[0] for c in candidates)  # contexts / buffers to allocate
     ctxs = []
     for _ in range(depth):
         c = P.Context(local)
@@ -284,24 +289,31 @@ def main():
 
     frame = None
     pending = [None] * depth  # per slot: (step, event after the frame's gather)
-    run = {"dn": depth, "warm": args.warmup, "kms": [], "rays": [], "exec": []}
+    run = {"dn": depth, "warm": args.warmup, "kms": [], "rays": [], "exec": [], "prm": prm,
+           "gate": False}
+    done = [torch.cuda.Event() for _ in range(depth)]  # per slot: after the frame's render
 
     def launch(step):
         nonlocal frame
         sl = step % run["dn"]
         ctx, st = ctxs[sl], streams[sl]
+        if run["gate"] and step >= 2 and run["dn"] >= 3:
+            st.wait_event(done[(step - 2) % run["dn"]])
         if world == 1:
-            ctx.render_device(prm, acc[sl].data_ptr(), rgb_rows[sl].data_ptr(), st.cuda_stream)
+            ctx.render_device(run["prm"], acc[sl].data_ptr(), rgb_rows[sl].data_ptr(), st.cuda_stream)
+            done[sl].record(st)
             frame = acc[sl]
             pending[sl] = (step, None)
             return
         if args.gather_fp64:
-            ctx.render_device(prm, acc[sl].data_ptr(), 0, st.cuda_stream)
+            ctx.render_device(run["prm"], acc[sl].data_ptr(), 0, st.cuda_stream)
+            done[sl].record(st)
             src = acc[sl]
         else:
             # write_color is per pixel: each rank quantises its own rows, and
             # the gather moves 3 B per pixel instead of 24 (C3: 2.9 MB, not 23)
-            ctx.render_device(prm, acc[sl].data_ptr(), rgb_rows[sl].data_ptr(), st.cuda_stream)
+            ctx.render_device(run["prm"], acc[sl].data_ptr(), rgb_rows[sl].data_ptr(), st.cuda_stream)
+            done[sl].record(st)
             src = rgb_rows[sl]
         comm.wait_stream(st)
         with torch.cuda.stream(comm):
@@ -335,10 +347,11 @@ def main():
             retire(k)
         torch.cuda.synchronize(dev)
 
-    def timed(dn, nwarm, nsteps):
+    def timed(dn, nwarm, nsteps, tail=True, gate=False):
         """nwarm untimed + nsteps timed frames, dn in flight; the timed frames
         start from an idle GPU and end when the last one is done."""
-        run.update(dn=dn, warm=nwarm, kms=[], rays=[], exec=[])
+        run.update(dn=dn, warm=nwarm, kms=[], rays=[], exec=[],
+                   prm=prm if tail else prm_notail, gate=gate)
         for step in range(nwarm + nsteps):
             if step == nwarm:
                 drain()
@@ -356,7 +369,25 @@ def main():
             el = float(t.item())
         return el
 
-    elapsed = timed(depth, args.warmup, args.steps)
+    # untimed tuning runs: every candidate (depth, tail priority) renders
+    # full frames; the fastest (max over ranks) is the one timed below
+    def cname(c):
+        return f"{c[0]}" + ("" if c[1] else "-notail") + ("-gated" if c[2] else "")
+    tuning = {}
+    if len(candidates) > 1:
+        for c in candidates:
+            nt = max(6, 2 * c[0])
+            tuning[cname(c)] = timed(c[0], 1, nt, c[1], c[2]) / nt * 1e3
+    # Frames in flight only for a clear gain (> 3% in the tuning runs): with
+    # C3's long frames the tail is worth ~2.5% at best, and a pipelined run
+    # can settle into a schedule where two traces share the GPU and lose more
+    # (DESIGN.md §7); C1 / C2 frames gain 8% to 2x
+    depth, tail_prio, gated = candidates[0]
+    if tuning:
+        best = min(candidates, key=lambda c: tuning[cname(c)])
+        if tuning[cname(best)] < 0.97 * tuning[cname(candidates[0])]:
+            depth, tail_prio, gated = best
+    elapsed = timed(depth, args.warmup, args.steps, tail_prio, gated)
     last_slot = (args.warmup + args.steps - 1) % depth
     if world == 1:
         rgb = rgb_rows[last_slot]
@@ -451,6 +482,9 @@ def main():
             },
             "rays_per_sample": round(float(np.sum(rays)) / (rows * w * spp * len(rays)), 3),
             "frames_in_flight": depth,
+            "tail_priority": tail_prio,
+            "gated": gated,
+            "depth_tuning_ms": {k: round(v, 3) for k, v in tuning.items()} or None,
             # the same frames rendered one at a time (each waits for the last)
             "unpipelined": unpiped,
         }

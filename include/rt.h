@@ -83,6 +83,9 @@ typedef struct {
 #define RT_FLAG_NONE 0
 #define RT_FLAG_NO_CULL 1u /* force the linear sphere sweep (no BVH): same bits, slower */
 #define RT_FLAG_NO_FIXPOINT 2u /* trace provably trapped paths to max_depth: same bits, slower */
+/* scheduling hint, same bits: the launch's draining waves do not take issue
+ * priority over other work (e.g. the next frame's launch on another stream) */
+#define RT_FLAG_NO_TAIL_PRIORITY 4u
 
 typedef struct {
   int width;      /* image_width  (main.cc:57)                              */

@@ -69,9 +69,14 @@ psrt::FastDiv fast_div_make(unsigned d) {
   return f;
 }
 
-// d_counters layout (words)
+// d_counters layout (words): [1, 5) totals (psrt_reduce), [8, 128) stamps
+constexpr size_t kTotals = 1;
 constexpr size_t kHeads = 128;
-constexpr size_t kSets = kHeads + (size_t)psrt::kQueues * psrt::kShardStride;
+#ifndef PSRT_SETS_SAME_LINE
+#define PSRT_SETS_SAME_LINE 0  // measurement: one head, its counter set on the head's line
+#endif
+constexpr size_t kSets =
+    kHeads + (PSRT_SETS_SAME_LINE ? 1 : (size_t)psrt::kQueues * psrt::kShardStride);
 constexpr size_t kCounterWords = kSets + (size_t)psrt::kQueues * psrt::kShardStride;
 
 size_t sample_buffer_cap_bytes() {
@@ -127,6 +132,12 @@ struct rt_context {
   // [8, 128) diagnostic stamps; queue heads at kHeads, statistics counter sets
   // (rays, sphere tests, box tests, traced rays) at kSets, kShardStride apart
   unsigned long long* d_counters = nullptr;
+  // The render's statistics, written by its last psrt_reduce straight into
+  // pinned host memory: reading them back needs no copy kernel, which (like
+  // any kernel) would wait for a free CU slot behind the next frame's
+  // persistent trace launch
+  unsigned long long* h_stats = nullptr;  // [4] host pointer
+  unsigned long long* d_stats = nullptr;  // the same memory, device pointer
   std::vector<hipEvent_t> ev;  // pairs around each trace launch
   int ev_used = 0;
   hipEvent_t ev_all0 = nullptr, ev_all1 = nullptr;
@@ -241,6 +252,13 @@ int rt_context_create(int device, rt_context** out) {
   }
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIP_TRY(hipMalloc(&c->d_counters, kCounterWords * sizeof(unsigned long long)));
+  // zeroed once: psrt_reduce leaves the queue heads and counter sets at zero
+  HIP_TRY(hipMemsetAsync(c->d_counters, 0, kCounterWords * sizeof(unsigned long long), c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipHostMalloc((void**)&c->h_stats, 4 * sizeof(unsigned long long),
+                        hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_TRY(hipHostGetDevicePointer((void**)&c->d_stats, c->h_stats, 0));
+  std::fill(c->h_stats, c->h_stats + 4, 0ull);
   HIP_TRY(hipEventCreate(&c->ev_all0));
   HIP_TRY(hipEventCreate(&c->ev_all1));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_plist, hipEventDisableTiming));
@@ -251,7 +269,8 @@ int rt_context_create(int device, rt_context** out) {
 int rt_context_destroy(rt_context* c) {
   if (!c) return RT_OK;
   (void)hipSetDevice(c->device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  (void)quiesce(c);
+  if (c->h_stats) (void)hipHostFree(c->h_stats);
   (void)hipFree(c->d_geo);
   (void)hipFree(c->d_inv_r);
   (void)hipFree(c->d_samples);
@@ -305,6 +324,10 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
     HIP_TRY(hipMalloc(&c->d_inv_r, cap * sizeof(double)));
     c->n_cap = cap;
   }
+  // uploads on the context's (non-blocking) stream; synchronised below
+  auto up = [c](void* dst, const void* src, size_t bytes) {
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream);
+  };
   // sphere.cc:11 radius*radius and vec3.h:151-154 1/t, each the same IEEE
   // product/quotient the reference forms per call.
   std::vector<double4> geo(cap);
@@ -314,8 +337,8 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
     inv[k] = 1 / sph[k].r;
   }
   if (n > 0) {
-    HIP_TRY(hipMemcpy(c->d_geo, geo.data(), n * sizeof(double4), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(c->d_inv_r, inv.data(), n * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(up(c->d_geo, geo.data(), n * sizeof(double4)));
+    HIP_TRY(up(c->d_inv_r, inv.data(), n * sizeof(double)));
   }
   c->n = n;
   c->cam = *cam;
@@ -355,33 +378,32 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
       dn[k].xy = make_float4(nd.lo[0], nd.lo[1], nd.hi[0], nd.hi[1]);
       dn[k].z = make_float4(nd.lo[2], nd.hi[2], sk, lf);
     }
-    HIP_TRY(hipMemcpy(c->d_nodes, dn.data(), dn.size() * sizeof(psrt::DevNode),
-                      hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(c->d_leaf_geo, lg.data(), lg.size() * sizeof(double4),
-                      hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(c->d_leaf_idx, b.leaf_idx.data(), b.leaf_idx.size() * sizeof(int),
-                      hipMemcpyHostToDevice));
+    HIP_TRY(up(c->d_nodes, dn.data(), dn.size() * sizeof(psrt::DevNode)));
+    HIP_TRY(up(c->d_leaf_geo, lg.data(), lg.size() * sizeof(double4)));
+    HIP_TRY(up(c->d_leaf_idx, b.leaf_idx.data(), b.leaf_idx.size() * sizeof(int)));
     if (c->n_big > 0)
-      HIP_TRY(hipMemcpy(c->d_big, b.big_idx.data(), b.big_idx.size() * sizeof(int),
-                        hipMemcpyHostToDevice));
+      HIP_TRY(up(c->d_big, b.big_idx.data(), b.big_idx.size() * sizeof(int)));
     c->pgrid = b.grid;
     c->pad = b.pad;
     const size_t ns = b.grid.start.size(), ni = std::max<size_t>(1, b.grid.items.size());
     HIP_TRY(hipMalloc(&c->d_cell_start, ns * sizeof(int)));
     HIP_TRY(hipMalloc(&c->d_cell_items, ni * sizeof(int)));
-    HIP_TRY(hipMemcpy(c->d_cell_start, b.grid.start.data(), ns * sizeof(int),
-                      hipMemcpyHostToDevice));
+    HIP_TRY(up(c->d_cell_start, b.grid.start.data(), ns * sizeof(int)));
     if (!b.grid.items.empty())
-      HIP_TRY(hipMemcpy(c->d_cell_items, b.grid.items.data(), b.grid.items.size() * sizeof(int),
-                        hipMemcpyHostToDevice));
+      HIP_TRY(up(c->d_cell_items, b.grid.items.data(), b.grid.items.size() * sizeof(int)));
     const size_t nw = b.nb_word.size(), nn = std::max<size_t>(1, b.nb_items.size());
     HIP_TRY(hipMalloc(&c->d_nb_word, std::max<size_t>(1, nw) * sizeof(int)));
     HIP_TRY(hipMalloc(&c->d_nb_items, nn * sizeof(int)));
-    if (nw) HIP_TRY(hipMemcpy(c->d_nb_word, b.nb_word.data(), nw * sizeof(int), hipMemcpyHostToDevice));
+    if (nw) HIP_TRY(up(c->d_nb_word, b.nb_word.data(), nw * sizeof(int)));
     if (!b.nb_items.empty())
-      HIP_TRY(hipMemcpy(c->d_nb_items, b.nb_items.data(), b.nb_items.size() * sizeof(int),
-                        hipMemcpyHostToDevice));
+      HIP_TRY(up(c->d_nb_items, b.nb_items.data(), b.nb_items.size() * sizeof(int)));
+    // the uploads above read host vectors of this block: wait for them here
+    HIP_TRY(hipStreamSynchronize(c->stream));
   }
+  // scene uploads run on the context's (non-blocking) stream; renders on it
+  // are ordered after them, and returning only once they are done orders
+  // renders on any other stream too
+  HIP_TRY(hipStreamSynchronize(c->stream));
   c->scene.assign(sph, sph + n);
   return RT_OK;
 }
@@ -429,7 +451,8 @@ static int check_params(const rt_params* p) {
                 p->row_stride, p->height);
   if ((long long)p->width * p->height >= (1LL << 32))
     return set_error(RT_E_INVALID, "image too large for 32-bit pixel ids");
-  if (p->flags & ~(RT_FLAG_NO_CULL | RT_FLAG_NO_FIXPOINT)) return set_error(RT_E_INVALID, "unknown flags 0x%x", p->flags);
+  if (p->flags & ~(RT_FLAG_NO_CULL | RT_FLAG_NO_FIXPOINT | RT_FLAG_NO_TAIL_PRIORITY))
+    return set_error(RT_E_INVALID, "unknown flags 0x%x", p->flags);
   return RT_OK;
 }
 
@@ -494,8 +517,10 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   // shared by its renders: a render on another stream than the last one
   // starts after it (same stream: stream order already does it).
   if (c->in_flight && st != c->last_stream) HIP_TRY(hipStreamWaitEvent(st, c->ev_all1, 0));
-  if (P == 0) {  // a shard that owns no rows: zero counters, no launch
-    HIP_TRY(hipMemsetAsync(c->d_counters, 0, kCounterWords * sizeof(unsigned long long), st));
+  if (P == 0) {  // a shard that owns no rows: zero statistics, no launch
+    const int qrc = quiesce(c);  // the last render's psrt_reduce writes h_stats
+    if (qrc) return qrc;
+    std::fill(c->h_stats, c->h_stats + 4, 0ull);
     HIP_TRY(hipEventRecord(c->ev_all0, st));
     HIP_TRY(hipEventRecord(c->ev_all1, st));
     c->in_flight = true;
@@ -545,12 +570,16 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   ta.row_stride = p->row_stride;
   ta.pixels = (unsigned)P;
   ta.seedmix = splitmix64_host(p->seed);
+  ta.tail_prio = !(p->flags & RT_FLAG_NO_TAIL_PRIORITY);
   ta.div_w = fast_div_make((unsigned)p->width);
   ta.work_counter = c->d_counters + kHeads;
   ta.ray_counter = c->d_counters + kSets;
 
-  HIP_TRY(hipMemsetAsync(c->d_counters, 0, kCounterWords * sizeof(unsigned long long), st));
+  // No memset here: the queue heads and counter sets are zero (context
+  // creation, then every psrt_reduce), and a small fill kernel on this stream
+  // would wait for a CU slot behind another frame's persistent launch.
   const bool stamps = std::getenv("PSRT_STAMPS") != nullptr;  // diagnostic build
+  if (stamps) HIP_TRY(hipMemsetAsync(c->d_counters + 8, 0, 120 * sizeof(unsigned long long), st));
   ta.stamps = c->d_counters + 8;
   ta.wave_log = nullptr;
   if (stamps) {
@@ -657,9 +686,6 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     ta.div_s = fast_div_make((unsigned)sc);
     ta.total_units = (uint64_t)P * sc;
     queue_phases(ta, use_bvh ? c->grid_bvh : c->grid, use_bvh);
-    if (ch > 0)  // the heads of the previous chunk's queue
-      HIP_TRY(hipMemsetAsync(c->d_counters + kHeads, 0,
-                             psrt::kQueues * psrt::kShardStride * sizeof(unsigned long long), st));
     HIP_TRY(hipEventRecord(c->ev[2 * ch], st));
     const double4* g4 = c->d_geo;
     const double* ir = c->d_inv_r;
@@ -695,6 +721,10 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     ra.spp_total = p->spp;
     ra.accum = acc;
     ra.rgb8 = (ch == nchunks - 1) ? d_rgb8 : nullptr;
+    ra.heads = c->d_counters + kHeads;
+    ra.sets = c->d_counters + kSets;
+    ra.totals = c->d_counters + kTotals;
+    ra.host_stats = (ch == nchunks - 1) ? c->d_stats : nullptr;
     const unsigned blocks = (unsigned)((P + psrt::kReduceBlock - 1) / psrt::kReduceBlock);
     hipLaunchKernelGGL(psrt::psrt_reduce, dim3(blocks), dim3(psrt::kReduceBlock), 0, st, ra);
     HIP_TRY(hipGetLastError());
@@ -716,15 +746,9 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   if (!c->in_flight) return set_error(RT_E_INVALID, "rt_context_sync_stats: no render enqueued");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipEventSynchronize(c->ev_all1));
-  unsigned long long sets[psrt::kQueues * psrt::kShardStride];
-  // on the render's own stream: a null-stream copy would also wait for work
-  // other contexts queued on other streams (a pipelined next frame)
-  HIP_TRY(hipMemcpyAsync(sets, c->d_counters + kSets, sizeof sets, hipMemcpyDeviceToHost,
-                         c->last_stream));
-  HIP_TRY(hipStreamSynchronize(c->last_stream));
-  unsigned long long cnt[4] = {0, 0, 0, 0};
-  for (int q = 0; q < psrt::kQueues; ++q)
-    for (int k = 0; k < 4; ++k) cnt[k] += sets[psrt::kShardStride * q + k];
+  // the render's last psrt_reduce wrote its totals into pinned host memory
+  unsigned long long cnt[4];
+  for (int k = 0; k < 4; ++k) cnt[k] = ((volatile unsigned long long*)c->h_stats)[k];
   const unsigned long long rays = cnt[0];
   double kms = 0.0;
   for (int ch = 0; ch < c->ev_used; ++ch) {
@@ -888,13 +912,15 @@ int rt_debug_probe_f64(int op, const double* x, const double* y, double* out, in
   HIP_TRY(hipMalloc(&dx, n * sizeof(double)));
   HIP_TRY(hipMalloc(&dy, n * sizeof(double)));
   HIP_TRY(hipMalloc(&dout, n * sizeof(double)));
-  HIP_TRY(hipMemcpy(dx, x, n * sizeof(double), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(dy, y, n * sizeof(double), hipMemcpyHostToDevice));
+  // every copy on the context's stream: it is non-blocking, so null-stream
+  // copies and memsets would not be ordered before the launch
+  HIP_TRY(hipMemcpyAsync(dx, x, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(dy, y, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
   hipLaunchKernelGGL(psrt::psrt_probe_f64, dim3((n + 255) / 256), dim3(256), 0, c->stream, op,
                      (const double*)dx, (const double*)dy, dout, (unsigned)n);
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out, dout, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  HIP_TRY(hipMemcpy(out, dout, n * sizeof(double), hipMemcpyDeviceToHost));
   (void)hipFree(dx);
   (void)hipFree(dy);
   (void)hipFree(dout);
@@ -921,18 +947,24 @@ int rt_debug_world_hit_hint(const rt_sphere* sph, int n, const double* rays, con
   int* dh = nullptr;
   HIP_TRY(hipMalloc(&dr, (size_t)count * 8 * sizeof(double)));
   HIP_TRY(hipMalloc(&dout, (size_t)count * 9 * sizeof(double)));
-  HIP_TRY(hipMemcpy(dr, rays, (size_t)count * 8 * sizeof(double), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemset(dout, 0, (size_t)count * 9 * sizeof(double)));
+  // every copy and the memset on the context's stream: it is non-blocking, so
+  // null-stream work would not be ordered before the launch (a null-stream
+  // memset of dout once raced with the kernel and zeroed part of its output)
+  HIP_TRY(hipMemcpyAsync(dr, rays, (size_t)count * 8 * sizeof(double), hipMemcpyHostToDevice,
+                         c->stream));
+  HIP_TRY(hipMemsetAsync(dout, 0, (size_t)count * 9 * sizeof(double), c->stream));
   if (hints) {
     HIP_TRY(hipMalloc(&dh, (size_t)count * sizeof(int)));
-    HIP_TRY(hipMemcpy(dh, hints, (size_t)count * sizeof(int), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpyAsync(dh, hints, (size_t)count * sizeof(int), hipMemcpyHostToDevice,
+                           c->stream));
   }
   hipLaunchKernelGGL(psrt::psrt_probe_hit, dim3((count + 63) / 64), dim3(64), 0, c->stream,
                      (const double4*)c->d_geo, (const double*)c->d_inv_r, n, (const double*)dr,
                      (const int*)dh, dout, (unsigned)count, bvh_view(c), (cull && c->bvh) ? 1 : 0);
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out, dout, (size_t)count * 9 * sizeof(double), hipMemcpyDeviceToHost,
+                         c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  HIP_TRY(hipMemcpy(out, dout, (size_t)count * 9 * sizeof(double), hipMemcpyDeviceToHost));
   (void)hipFree(dr);
   (void)hipFree(dout);
   (void)hipFree(dh);

@@ -94,6 +94,7 @@ struct TraceArgs {
   unsigned walk_tail;               // a BVH pass stops once this few lanes still walk
   FastDiv div_s, div_w;             // unit / s_count, q / width
   unsigned flush_at;                // per-lane counters flush to the totals at this value
+  int tail_prio;                    // raise the issue priority of waves whose queue is empty
 };
 
 // BVH node as the device reads it (two float4, from psrt_bvh.h BvhNode):
@@ -151,6 +152,14 @@ struct ReduceArgs {
   int spp_total;
   double* accum;          // [pixels][3] (required unless single chunk + rgb only)
   unsigned char* rgb8;    // [pixels][3] or nullptr (last chunk only)
+  // Statistics and queue state of the trace launch before this reduce
+  // (block 0 only): the counter sets are added into totals (reset on the first
+  // chunk), then the sets and the queue heads are zeroed for the next launch;
+  // the last chunk also writes totals to host_stats (pinned host memory).
+  unsigned long long* heads;       // TraceArgs::work_counter (kQueues heads)
+  unsigned long long* sets;        // TraceArgs::ray_counter (kQueues sets)
+  unsigned long long* totals;      // [4], device
+  unsigned long long* host_stats;  // [4], or nullptr
 };
 
 template <bool kBVH, bool kStamps, bool kLds>

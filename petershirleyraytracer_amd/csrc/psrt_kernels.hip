@@ -1003,6 +1003,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   uint64_t win_base = 0;
   unsigned win_left = 0;
   bool exhausted = false;
+  bool tailp = false;  // exhausted, and the launch's tail runs at PSRT_TAIL_PRIO (a.tail_prio)
 
   bool active = false;
   bool done = false;  // sample finished; its colour is stored by the next refill block
@@ -1183,7 +1184,10 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
         exhausted = true;
         // Launch tail: this wave's remaining paths decide when the launch
         // (and the next frame's start on its CUs) ends; let them issue first.
-        if constexpr (PSRT_TAIL_PRIO > 0) __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
+        if (PSRT_TAIL_PRIO > 0 && a.tail_prio) {
+          tailp = true;
+          __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
+        }
         if constexpr (kStamps) {
           const unsigned long long t = __builtin_amdgcn_s_memrealtime();
           if (wlog && lane == 0) wlog[1] = t, wlog[3] = iters;
@@ -1191,7 +1195,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       }
     }
     if constexpr (PSRT_REFILL_PRIO > 0) {
-      if (PSRT_TAIL_PRIO > 0 && exhausted) __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
+      if (PSRT_TAIL_PRIO > 0 && tailp) __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
       else __builtin_amdgcn_s_setprio(0);
     }
     clk.mark(kSecRefill);
@@ -1260,7 +1264,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       }
     }
     if constexpr (PSRT_HIT_PRIO > 0) {  // back to the base priority
-      if (PSRT_TAIL_PRIO > 0 && exhausted) __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
+      if (PSRT_TAIL_PRIO > 0 && tailp) __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
       else __builtin_amdgcn_s_setprio(0);
     }
     clk.mark(kSecHit);
@@ -1299,7 +1303,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
           }
         }
         if constexpr (PSRT_WALK_PRIO > 0) {
-          if (PSRT_TAIL_PRIO > 0 && exhausted) __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
+          if (PSRT_TAIL_PRIO > 0 && tailp) __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
           else __builtin_amdgcn_s_setprio(0);
         }
       }
@@ -1422,7 +1426,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       ++k;
     }
     if constexpr (PSRT_SCATTER_PRIO > 0) {
-      if (PSRT_TAIL_PRIO > 0 && exhausted) __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
+      if (PSRT_TAIL_PRIO > 0 && tailp) __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
       else __builtin_amdgcn_s_setprio(0);
     }
     clk.mark(kSecScatter);
@@ -1479,6 +1483,21 @@ PSRT_INSTANTIATE(true, true, true)
 
 __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
   if constexpr (PSRT_REDUCE_PRIO > 0) __builtin_amdgcn_s_setprio(PSRT_REDUCE_PRIO);
+  // the trace launch's sharded counter sets -> totals (-> host), then the
+  // sets and queue heads back to zero (ReduceArgs; stream order puts this
+  // after every trace block and before the context's next launch)
+  if (blockIdx.x == 0) {
+    if (threadIdx.x < 4) {
+      unsigned long long v = a.first_chunk ? 0ull : a.totals[threadIdx.x];
+      for (int h = 0; h < kQueues; ++h) {
+        v += a.sets[kShardStride * h + threadIdx.x];
+        a.sets[kShardStride * h + threadIdx.x] = 0ull;
+      }
+      a.totals[threadIdx.x] = v;
+      if (a.host_stats) a.host_stats[threadIdx.x] = v;
+    }
+    if (threadIdx.x < kQueues) a.heads[kShardStride * threadIdx.x] = 0ull;
+  }
   // One wave per 64 pixels. A pixel's samples are contiguous, so the wave
   // stages [64 pixels][kReduceTile samples] tiles through LDS, then each lane
   // adds its pixel's samples in order.

@@ -50,6 +50,7 @@ def _camera_array(c: RtCamera) -> np.ndarray:
 
 FLAG_NO_CULL = 1
 FLAG_NO_FIXPOINT = 2  # trace provably trapped paths to max_depth (same bits, slower)
+FLAG_NO_TAIL_PRIORITY = 4  # scheduling hint: no issue priority for the launch tail (same bits)
 
 
 def params(width: int, height: int, spp: int, max_depth: int = 50, seed: int = 0,

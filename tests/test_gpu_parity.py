@@ -266,3 +266,33 @@ def test_context_device_buffers(oracle_mod):
     torch.cuda.synchronize()
     assert torch.equal(rgb2, rgb)
     ctx.close()
+
+
+def test_context_repeat_renders_stats(oracle_mod, monkeypatch):
+    """Renders on one context leave its queue heads and counter sets at zero
+    (psrt_reduce resets them; no memset in the render's stream): repeated
+    renders, RT_FLAG_NO_TAIL_PRIORITY and a multi-chunk render all give the
+    same bits and the same statistics."""
+    import torch
+    from petershirleyraytracer_amd.render import FLAG_NO_TAIL_PRIORITY
+    sph = oracle_mod.scene_random_spheres(1)
+    cam = oracle_mod.camera_look_at(aspect=120 / 80)
+    ctx = P.Context(0)
+    ctx.set_scene(sph, cam)
+    acc = torch.zeros((80, 120, 3), dtype=torch.float64, device="cuda:0")
+    rgb = torch.zeros((80, 120, 3), dtype=torch.uint8, device="cuda:0")
+    s = ctx.stream()
+    keys = ("rays", "tests_executed", "box_tests", "rays_traced")
+    runs = []
+    for flags, buf_mb in ((0, None), (0, None), (FLAG_NO_TAIL_PRIORITY, None), (0, "1")):
+        if buf_mb:
+            monkeypatch.setenv("PSRT_SAMPLE_BUF_MB", buf_mb)  # 9600 px x 10 B: 8-sample chunks
+        ctx.render_device(P.params(120, 80, 300, flags=flags), acc.data_ptr(), rgb.data_ptr(), s)
+        st = ctx.sync_stats()
+        torch.cuda.synchronize()
+        runs.append((bits(acc.cpu().numpy()), rgb.cpu().numpy(), {k: st[k] for k in keys}))
+    for a, r, st in runs[1:]:
+        assert np.array_equal(a, runs[0][0]) and np.array_equal(r, runs[0][1])
+        assert st == runs[0][2]
+    assert runs[0][2]["rays"] > 0 and runs[0][2]["box_tests"] > 0
+    ctx.close()
