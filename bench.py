@@ -94,6 +94,8 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=0,
                     help="frames in flight (1 = each frame waits for the previous one; "
                          "0 = auto: 1 for multi-chunk frames, else 3)")
+    ap.add_argument("--gate", action="store_true",
+                    help="with --pipeline >= 3: frame k's trace waits on the device for frame k-2")
     ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
                     help="weak: N GPUs render the frame at N x spp (per-GPU work fixed); "
                          "strong: the configured frame on any N")
@@ -259,15 +261,15 @@ def main():
     # picked by measurement on this GPU (`tuning` below, untimed runs).
     per_rank = rows * w * spp
     buf_cap = int(os.environ.get("PSRT_SAMPLE_BUF_MB", "16384")) << 20  # psrt_capi.hip
-    # candidates: (frames in flight, tail priority, gated): gated = a frame's
-    # trace waits on the device for frame - 2 to finish, so that at most two
-    # traces are in flight and the next one fills only the running one's tail
+    # candidates: (frames in flight, tail priority, gated); gated = a frame's
+    # trace waits on the device for frame - 2 to finish (--gate; measured, no
+    # better than ungated: DESIGN.md §7)
     if args.pipeline > 0:
-        candidates = [(args.pipeline, True, False)]
+        candidates = [(args.pipeline, True, args.gate)]
     elif per_rank * SAMPLE_RECORD_BYTES > buf_cap:
         candidates = [(1, True, False)]
     else:
-        candidates = [(1, True, False), (2, True, False), (3, True, False), (3, True, True)]
+        candidates = [(1, True, False), (2, True, False), (3, True, False)]
     depth = max(c[0] for c in candidates)  # contexts / buffers to allocate
     ctxs = []
     for _ in range(depth):
