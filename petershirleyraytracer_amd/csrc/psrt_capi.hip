@@ -472,7 +472,10 @@ static int check_params(const rt_params* p) {
 static void queue_phases(psrt::TraceArgs& ta, int grid, bool guided) {
   const char* ek = std::getenv("PSRT_QUEUE_K");
   const char* ed = std::getenv("PSRT_QUEUE_D");
-  const double k = ek ? std::atof(ek) : 1.0;
+  // two tickets per resident wave per phase for large launches: C3 (96 M
+  // units) one frame at a time 13.64 -> 13.56 ms per step; a strong 1/8
+  // shard (12 M units, frames in flight) prefers one (1.96 vs 1.97 ms)
+  const double k = ek ? std::atof(ek) : (ta.total_units >= (32ull << 20) ? 2.0 : 1.0);
   const double d = ed ? std::atof(ed) : 4.0;  // 8 before frame pipelining (bench.py)
   const uint64_t waves = (uint64_t)grid * (psrt::kTraceBlock / 64);
   unsigned s0 = guided ? psrt::kWorkChunk : psrt::kLinearChunk;
