@@ -1477,6 +1477,9 @@ PSRT_INSTANTIATE(true, true, true)
 
 // pixel_color += sample, in sample order (main.cc:77-84); write_color on the
 // last chunk (color.h:8-24).
+#ifndef PSRT_REDUCE_PREFETCH
+#define PSRT_REDUCE_PREFETCH 1  // psrt_reduce: next tile's loads in flight while summing
+#endif
 #ifndef PSRT_REDUCE_PRIO
 #define PSRT_REDUCE_PRIO 0  // s_setprio of psrt_reduce's waves (they share CUs with the next frame's trace)
 #endif
@@ -1513,20 +1516,29 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
     g = a.accum[(size_t)q * 3 + 1];
     b = a.accum[(size_t)q * 3 + 2];
   }
-  for (unsigned s0 = 0; s0 < S; s0 += kReduceTile) {
-    const unsigned T = min((unsigned)kReduceTile, S - s0);
-    // Runs of a tile: kReduceTile doubles of t and kReduceTile uint16 of k
-    // per pixel. With s_count % 4 == 0 they are 16-B aligned: t is read in
-    // 16-B pieces (kLT lanes per pixel), k in 8-B pieces (kLK lanes per
-    // pixel); else element by element. Every load of a pass is in flight
-    // before the first LDS store.
-    constexpr int kLT = kReduceTile / 2, kPT = 64 / kLT;  // t: lanes, pixels per load
-    constexpr int kLK = kReduceTile / 4, kPK = 64 / kLK;  // k: lanes, pixels per load
-    static_assert(kReduceBlock == 64 && (kReduceTile == 16 || kReduceTile == 32),
-                  "tile shape of the loads below");
-    if (S % 4 == 0) {
-      double2 vt[kLT];
-      uint2 vk[kLK];
+  // Tiles of a pixel run: kReduceTile doubles of t and kReduceTile uint16 of
+  // k per pixel. With s_count % 4 == 0 they are 16-B aligned: t is read in
+  // 16-B pieces (kLT lanes per pixel), k in 8-B pieces (kLK lanes per pixel),
+  // and the next tile's loads are in flight while this tile is summed from
+  // LDS (PSRT_REDUCE_PREFETCH); else element by element.
+  constexpr int kLT = kReduceTile / 2, kPT = 64 / kLT;  // t: lanes, pixels per load
+  constexpr int kLK = kReduceTile / 4, kPK = 64 / kLK;  // k: lanes, pixels per load
+  static_assert(kReduceBlock == 64 && (kReduceTile == 16 || kReduceTile == 32),
+                "tile shape of the loads below");
+  auto sum_tile = [&](unsigned T) {
+    for (unsigned j = 0; j < T; ++j) {
+      double cr, cg, cb;
+      sample_colour(s_t[lane][j], s_k[lane][j], cr, cg, cb);
+      r += cr;
+      g += cg;
+      b += cb;
+    }
+  };
+  if (S % 4 == 0) {
+    double2 vt[kLT];
+    uint2 vk[kLK];
+    auto load = [&](unsigned s0) {
+      const unsigned T = min((unsigned)kReduceTile, S - s0);
 #pragma unroll
       for (int i = 0; i < kLT; ++i) {
         const unsigned p = kPT * i + lane / kLT, j = (lane % kLT) * 2;
@@ -1541,6 +1553,9 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
         if (q0 + p < a.pixels && j < T)
           vk[i] = *(const uint2*)(a.samp_k + (size_t)(q0 + p) * S + s0 + j);
       }
+    };
+    load(0);
+    for (unsigned s0 = 0; s0 < S; s0 += kReduceTile) {
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < kLT; ++i)
@@ -1548,7 +1563,14 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
 #pragma unroll
       for (int i = 0; i < kLK; ++i)
         *(uint2*)&s_k[kPK * i + lane / kLK][(lane % kLK) * 4] = vk[i];
-    } else {
+      __syncthreads();
+      if (PSRT_REDUCE_PREFETCH && s0 + kReduceTile < S) load(s0 + kReduceTile);
+      sum_tile(min((unsigned)kReduceTile, S - s0));
+      if (!PSRT_REDUCE_PREFETCH && s0 + kReduceTile < S) load(s0 + kReduceTile);
+    }
+  } else {
+    for (unsigned s0 = 0; s0 < S; s0 += kReduceTile) {
+      const unsigned T = min((unsigned)kReduceTile, S - s0);
       constexpr int kPP = 64 / kReduceTile;  // pixels per load
       double vt[8];
       unsigned short vk[8];
@@ -1568,14 +1590,8 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
           s_k[8 * kPP * h + kPP * i + lane / kReduceTile][lane % kReduceTile] = vk[i];
         }
       }
-    }
-    __syncthreads();
-    for (unsigned j = 0; j < T; ++j) {
-      double cr, cg, cb;
-      sample_colour(s_t[lane][j], s_k[lane][j], cr, cg, cb);
-      r += cr;
-      g += cg;
-      b += cb;
+      __syncthreads();
+      sum_tile(T);
     }
   }
   if (q >= a.pixels) return;
