@@ -167,6 +167,7 @@ def cpu_baseline(cfg, args, frame_acc):
             psnr = "inf" if mse == 0 else round(10 * math.log10(255.0 ** 2 / mse), 3)
             parity = dict(pixels_compared=n_pix, fp64_bit_identical=equal, ppm_psnr_db=psnr)
     cb = dict(value=samples / wall / 1e6, unit="Msamples/s", cores=procs, kind="reference",
+              per_process_value=samples / wall / 1e6 / procs,  # one core's share (1 thread each)
               sample=(f"{rows} rows (every {stride}th) x {w} cols x {spp_eff} spp "
                       f"= {samples} samples of the same workload; reference sources "
                       f"(g++ -O2, unmodified) in {procs} single-thread processes, "
