@@ -72,11 +72,7 @@ psrt::FastDiv fast_div_make(unsigned d) {
 // d_counters layout (words): [1, 5) totals (psrt_reduce), [8, 128) stamps
 constexpr size_t kTotals = 1;
 constexpr size_t kHeads = 128;
-#ifndef PSRT_SETS_SAME_LINE
-#define PSRT_SETS_SAME_LINE 0  // measurement: one head, its counter set on the head's line
-#endif
-constexpr size_t kSets =
-    kHeads + (PSRT_SETS_SAME_LINE ? 1 : (size_t)psrt::kQueues * psrt::kShardStride);
+constexpr size_t kSets = kHeads + (size_t)psrt::kQueues * psrt::kShardStride;
 constexpr size_t kCounterWords = kSets + (size_t)psrt::kQueues * psrt::kShardStride;
 
 size_t sample_buffer_cap_bytes() {
