@@ -261,13 +261,15 @@ def main():
     # several sample chunks runs alone (depth 1). Otherwise the depth is
     # picked by measurement on this GPU (`tuning` below, untimed runs).
     per_rank = rows * w * spp
-    buf_cap = int(os.environ.get("PSRT_SAMPLE_BUF_MB", "16384")) << 20  # psrt_capi.hip
+    buf_cap = int(os.environ.get("PSRT_SAMPLE_BUF_MB", "49152")) << 20  # psrt_capi.hip
     # candidates: (frames in flight, tail priority, gated); gated = a frame's
     # trace waits on the device for frame - 2 to finish (--gate; measured, no
     # better than ungated: DESIGN.md §7)
     if args.pipeline > 0:
         candidates = [(args.pipeline, True, args.gate)]
-    elif per_rank * SAMPLE_RECORD_BYTES > buf_cap:
+    elif per_rank * SAMPLE_RECORD_BYTES > buf_cap or per_rank >= (1 << 30):
+        # several sample chunks, or a frame so long (C4 on one GPU: 560 ms)
+        # that its ~0.5 ms tail is noise: one frame at a time, no tuning runs
         candidates = [(1, True, False)]
     else:
         candidates = [(1, True, False), (2, True, False), (3, True, False)]
