@@ -221,6 +221,26 @@ def test_multi_chunk_large_spp(oracle_mod, tmp_path):
     assert np.array_equal(bits(got), bits(want))
 
 
+def test_units_per_launch_limit(oracle_mod, monkeypatch):
+    """A shard of more than 2^32 samples (1024 x 1024 at 4100 spp): the
+    sample chunks are bounded by the 32-bit unit ids, not by the buffer, and
+    balanced (2 x ~2050 samples). The frame must not depend on how the
+    samples are chunked (14 chunks on a 3000 MB buffer), and its first row
+    must equal the oracle's."""
+    two = oracle_mod.scene_two_spheres()
+    cam = oracle_mod.camera_default()
+    w, h, spp = 1024, 1024, 4100
+    assert w * h * spp > 2**32
+    monkeypatch.delenv("PSRT_SAMPLE_BUF_MB", raising=False)
+    big, _, st_big = P.render(two, cam, w, h, spp)
+    monkeypatch.setenv("PSRT_SAMPLE_BUF_MB", "3000")
+    small, _, st_small = P.render(two, cam, w, h, spp)
+    assert np.array_equal(bits(big), bits(small))
+    assert st_big["rays"] == st_small["rays"]
+    want, _, _ = oracle_mod.render(two, cam, w, h, spp, row_offset=0, row_stride=h, threads=16)
+    assert np.array_equal(bits(big[:1]), bits(want))
+
+
 def test_edge_cases_vs_oracle(oracle_mod):
     two = oracle_mod.scene_two_spheres()
     cam = oracle_mod.camera_default()
