@@ -32,7 +32,7 @@ constexpr int kShardStride = 16;       // u64 words between heads / counter sets
 // float4 each, plus the padding node), spheres {c, r*r}, 1/r, leaf slots and
 // neighbour words; byte offsets, 16-B aligned. The host stages them when as
 // many workgroups per CU stay resident as without (C3: 573 nodes, 485
-// spheres, 41.6 KB; three workgroups, and psrt_reduce's 22 KB beside them).
+// spheres, 41.6 KB; three workgroups).
 struct LdsLayout {
   unsigned nodes, geo, inv, leaf, nb, bytes;
 };
