@@ -941,6 +941,18 @@ __device__ __forceinline__ void flush_counters(unsigned long long* ctr, unsigned
   }
 }
 
+// PSRT_BLOCK_DONE measurement builds: add n finished records to 64-pixel block
+// b's counter; the adder that completes the block (ub records) zeroes it.
+__device__ __forceinline__ void block_done_add(const TraceArgs& a, unsigned b, unsigned n) {
+  const unsigned ub = min(64u, a.pixels - 64u * b) * (unsigned)a.s_count;
+  if (PSRT_BLOCK_DONE & 8) {  // no return value: the atomic's issue cost alone
+    __hip_atomic_fetch_add(a.block_done + b, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (__hip_atomic_fetch_add(a.block_done + b, n, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT) + n == ub) {
+    __hip_atomic_store(a.block_done + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 template <bool kBVH, bool kStamps, bool kLds>
 __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(const double4* __restrict__ geo,
                                                           const double* __restrict__ inv_r,
@@ -999,6 +1011,8 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   const int* __restrict__ lleaf = (kLds && PSRT_LDS_LEAVES) ? s_leaf : bv.leaf_idx;
   const int* __restrict__ lnb = kLds ? s_nb : bv.nb_word;
 
+  // PSRT_BLOCK_DONE & 16: this wave's pending record counts of two blocks
+  [[maybe_unused]] unsigned agg_b0 = ~0u, agg_n0 = 0, agg_b1 = ~0u, agg_n1 = 0;
   // wave-uniform work window
   uint64_t win_base = 0;
   unsigned win_left = 0;
@@ -1071,6 +1085,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
         rays = cs.spheres = cs.boxes = 0u;
       }
       // sky (main.cc:46-48) x 0.5^k, or black; store
+      [[maybe_unused]] const bool stored = done;
       if (done) {
         // The colour is a function of (t, k) alone (sample_colour): store those
         // (10 B) in unit order. A wave's window is a run of consecutive units,
@@ -1084,7 +1099,13 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
           kk = (unsigned short)(k < kSampleKCap ? k : kSampleKCap);
         }
         const unsigned u = su;  // < total < 2^32
-#if PSRT_NT_STORE
+#if PSRT_BLOCK_DONE & 1
+        // agent-scope stores (global_store ... sc1): visible to a reducer on
+        // another XCD after its acquire (scripts/sc1_probe.hip)
+        __hip_atomic_store(samples + u, tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((unsigned short*)(samples + total) + u, kk, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+#elif PSRT_NT_STORE
         __builtin_nontemporal_store(tt, samples + u);
         __builtin_nontemporal_store(kk, (unsigned short*)(samples + total) + u);
 #else
@@ -1093,6 +1114,41 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
 #endif
         done = false;
       }
+#if PSRT_BLOCK_DONE & 4
+      // Per-block completion accounting of the in-launch reduce (DESIGN.md
+      // §13), measured alone: the records above complete, then one agent-scope
+      // atomic per distinct 64-pixel block among the lanes that stored; the
+      // lane that completes a block zeroes its counter (no reduce yet).
+      {
+        uint64_t m = __ballot(stored);
+        if (m != 0) {
+          if (PSRT_BLOCK_DONE & 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          const unsigned blk = q >> 6;  // 64-pixel block of this lane's record
+          while (m != 0) {
+            const int l0 = __builtin_ctzll(m);
+            const unsigned b0 = __shfl(blk, l0);
+            const uint64_t mine = __ballot(stored && blk == b0);
+            const unsigned n = (unsigned)__popcll(mine);
+            if (PSRT_BLOCK_DONE & 16) {
+              // per-wave aggregation over the (at most two) blocks the wave's
+              // windows currently cover: one atomic when a block leaves the pair
+              if (b0 == agg_b0) {
+                agg_n0 += n;
+              } else if (b0 == agg_b1) {
+                agg_n1 += n;
+              } else {
+                if (lane == 0 && agg_n0) block_done_add(a, agg_b0, agg_n0);
+                agg_b0 = agg_b1, agg_n0 = agg_n1;
+                agg_b1 = b0, agg_n1 = n;
+              }
+            } else if (lane == (unsigned)l0) {
+              block_done_add(a, b0, n);
+            }
+            m &= ~mine;
+          }
+        }
+      }
+#endif
     }
     if constexpr (PSRT_REFILL_PRIO > 0) {
       if (run_block && !exhausted) __builtin_amdgcn_s_setprio(PSRT_REFILL_PRIO);
@@ -1456,6 +1512,10 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   }
 
   if (PSRT_ABLATE && ablate_sink == 0x9E3779B9u && a.width < 0) samples[0] = ablate_sink;
+#if PSRT_BLOCK_DONE & 16
+  if (lane == 0 && agg_n0) block_done_add(a, agg_b0, agg_n0);
+  if (lane == 0 && agg_n1) block_done_add(a, agg_b1, agg_n1);
+#endif
   unsigned long long* const ctr = a.ray_counter + kShardStride * (blockIdx.x % kQueues);
   flush_counters(ctr, rays, cs.spheres, cs.boxes, lane);
   if (lane == 0 && traced) atomicAdd(ctr + 3, traced);
