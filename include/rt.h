@@ -86,6 +86,10 @@ typedef struct {
 /* scheduling hint, same bits: the launch's draining waves do not take issue
  * priority over other work (e.g. the next frame's launch on another stream) */
 #define RT_FLAG_NO_TAIL_PRIORITY 4u
+/* count the sphere / box tests the device runs (rt_stats.tests_executed,
+ * box_tests) with a slower kernel variant (~1%); without it both read 0.
+ * Same bits; every other counter is always exact. */
+#define RT_FLAG_CULL_STATS 8u
 
 typedef struct {
   int width;      /* image_width  (main.cc:57)                              */
@@ -103,8 +107,9 @@ typedef struct {
   uint64_t samples;        /* camera samples traced                          */
   uint64_t rays;           /* ray_color() invocations that called world.hit  */
   uint64_t sphere_tests;   /* sphere::hit calls of the reference = rays * n  */
-  uint64_t tests_executed; /* FP64 sphere tests the device ran (culled)      */
-  uint64_t box_tests;      /* FP32 BVH box tests the device ran              */
+  uint64_t tests_executed; /* FP64 sphere tests the device ran (culled);
+                              0 without RT_FLAG_CULL_STATS                   */
+  uint64_t box_tests;      /* FP32 BVH box tests the device ran (same)       */
   double kernel_ms;        /* device time of the trace kernels (HIP events)  */
   double total_ms;         /* device time of the whole render                */
   uint64_t rays_traced;    /* of `rays`, those the device traced; the rest

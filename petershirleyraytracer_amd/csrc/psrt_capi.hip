@@ -14,6 +14,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/rt.h"
@@ -233,17 +234,17 @@ int rt_context_create(int device, rt_context** out) {
   HIP_TRY(hipGetDeviceProperties(&prop, device));
   c->cus = prop.multiProcessorCount;
   int per_cu = 0;
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace<false, false, false>,
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace<false, false, false, false>,
                                                         psrt::kTraceBlock, 0));
   c->grid = c->cus * (per_cu < 1 ? 1 : per_cu);
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace<true, false, false>,
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace<true, false, false, false>,
                                                         psrt::kTraceBlock, 0));
   c->grid_bvh = c->cus * (per_cu < 1 ? 1 : per_cu);
   // the staged-scene variant keeps that residency up to lds_max bytes of
   // dynamic LDS (largest multiple of 256 B the occupancy query accepts)
   for (unsigned b = 65536; b >= 256; b -= 256) {
     int pc = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, psrt::psrt_trace<true, false, true>,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, psrt::psrt_trace<true, false, true, false>,
                                                      psrt::kTraceBlock, b) == hipSuccess &&
         pc >= per_cu) {
       c->lds_max = b;
@@ -452,7 +453,8 @@ static int check_params(const rt_params* p) {
                 p->row_stride, p->height);
   if ((long long)p->width * p->height >= (1LL << 32))
     return set_error(RT_E_INVALID, "image too large for 32-bit pixel ids");
-  if (p->flags & ~(RT_FLAG_NO_CULL | RT_FLAG_NO_FIXPOINT | RT_FLAG_NO_TAIL_PRIORITY))
+  if (p->flags &
+      ~(RT_FLAG_NO_CULL | RT_FLAG_NO_FIXPOINT | RT_FLAG_NO_TAIL_PRIORITY | RT_FLAG_CULL_STATS))
     return set_error(RT_E_INVALID, "unknown flags 0x%x", p->flags);
   return RT_OK;
 }
@@ -725,15 +727,23 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
       hipLaunchKernelGGL(kern, dim3(grid), blk, lds ? lds_bytes : 0, st, g4, ir, c->d_samples, ta,
                          bv);
     };
+    // RT_FLAG_CULL_STATS: the variant that counts sphere / box tests
+    auto pick = [&](auto kBVH, auto kStamps, auto kLds, int grid) {
+      if (p->flags & RT_FLAG_CULL_STATS)
+        launch(psrt::psrt_trace<decltype(kBVH)::value, decltype(kStamps)::value,
+                                decltype(kLds)::value, true>, grid);
+      else
+        launch(psrt::psrt_trace<decltype(kBVH)::value, decltype(kStamps)::value,
+                                decltype(kLds)::value, false>, grid);
+    };
+    using T = std::true_type;
+    using F = std::false_type;
     if (!use_bvh)
-      stamps ? launch(psrt::psrt_trace<false, true, false>, c->grid)
-             : launch(psrt::psrt_trace<false, false, false>, c->grid);
+      stamps ? pick(F{}, T{}, F{}, c->grid) : pick(F{}, F{}, F{}, c->grid);
     else if (lds)
-      stamps ? launch(psrt::psrt_trace<true, true, true>, c->grid_bvh)
-             : launch(psrt::psrt_trace<true, false, true>, c->grid_bvh);
+      stamps ? pick(T{}, T{}, T{}, c->grid_bvh) : pick(T{}, F{}, T{}, c->grid_bvh);
     else
-      stamps ? launch(psrt::psrt_trace<true, true, false>, c->grid_bvh)
-             : launch(psrt::psrt_trace<true, false, false>, c->grid_bvh);
+      stamps ? pick(T{}, T{}, F{}, c->grid_bvh) : pick(T{}, F{}, F{}, c->grid_bvh);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[2 * ch + 1], st));
     psrt::ReduceArgs ra{};

@@ -170,7 +170,7 @@ struct ReduceArgs {
   unsigned long long* host_stats;  // [4], or nullptr
 };
 
-template <bool kBVH, bool kStamps, bool kLds>
+template <bool kBVH, bool kStamps, bool kLds, bool kCount>
 __global__ void psrt_trace(const double4* __restrict__ geo, const double* __restrict__ inv_r,
                            double* __restrict__ samples, TraceArgs a, BvhView bv);
 __global__ void psrt_reduce(ReduceArgs a);

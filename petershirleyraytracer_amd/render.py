@@ -51,6 +51,7 @@ def _camera_array(c: RtCamera) -> np.ndarray:
 FLAG_NO_CULL = 1
 FLAG_NO_FIXPOINT = 2  # trace provably trapped paths to max_depth (same bits, slower)
 FLAG_NO_TAIL_PRIORITY = 4  # scheduling hint: no issue priority for the launch tail (same bits)
+FLAG_CULL_STATS = 8  # count executed sphere / box tests (slower kernel variant; else they read 0)
 
 
 def params(width: int, height: int, spp: int, max_depth: int = 50, seed: int = 0,
@@ -153,11 +154,13 @@ def stats_dict(s: RtStats) -> dict:
 
 def render(spheres, camera, width: int, height: int, spp: int, max_depth: int = 50,
            seed: int = 0, row_offset: int = 0, row_stride: int = 1, want_rgb: bool = True,
-           cull: bool = True, fixpoint: bool = True):
+           cull: bool = True, fixpoint: bool = True, cull_stats: bool = False):
     """One-shot render of the owned rows on the default device (RT_DEVICE).
 
     cull=False forces the linear sweep; fixpoint=False traces provably trapped
     paths to max_depth. Neither changes a bit of the output.
+    cull_stats=True counts the executed sphere / box tests (tests_executed,
+    box_tests; 0 otherwise) with the slower counting kernel, same bits.
 
     Returns (accum[rows, W, 3] float64, rgb8[rows, W, 3] uint8 or None, stats dict).
     """
@@ -165,7 +168,8 @@ def render(spheres, camera, width: int, height: int, spp: int, max_depth: int = 
     sp, n = _spheres(spheres)
     cam = _camera(camera)
     p = params(width, height, spp, max_depth, seed, row_offset, row_stride,
-               (0 if cull else FLAG_NO_CULL) | (0 if fixpoint else FLAG_NO_FIXPOINT))
+               (0 if cull else FLAG_NO_CULL) | (0 if fixpoint else FLAG_NO_FIXPOINT)
+               | (FLAG_CULL_STATS if cull_stats else 0))
     # a shard that owns no rows (row_offset >= height: more ranks than rows)
     # renders nothing and returns empty [0, W, 3] blocks
     rows = max(0, L.rt_rows_owned(height, row_offset, row_stride))

@@ -103,9 +103,9 @@ def test_counter_flush_keeps_totals(oracle_mod, monkeypatch, flush_at):
     for key, (s, c, w, h, n, d) in {"two": (two, cam, 40, 20, 3, 100000),
                                      "fin": (fin, cam_f, 48, 32, 4, 50)}.items():
         monkeypatch.delenv("PSRT_FLUSH_AT", raising=False)
-        acc0, _, st0 = P.render(s, c, w, h, n, d)
+        acc0, _, st0 = P.render(s, c, w, h, n, d, cull_stats=True)
         monkeypatch.setenv("PSRT_FLUSH_AT", flush_at)
-        acc1, _, st1 = P.render(s, c, w, h, n, d)
+        acc1, _, st1 = P.render(s, c, w, h, n, d, cull_stats=True)
         assert np.array_equal(bits(acc0), bits(acc1)), key
         for f in ("rays", "tests_executed", "box_tests", "rays_traced"):
             assert st0[f] == st1[f], (key, f)

@@ -208,11 +208,16 @@ def test_far_origins_inside_a_huge_ground():
 
 def test_renders_cull_equals_no_cull(oracle_mod, final_scene):
     cam = P.camera_look_at(aspect=160 / 90)
-    a, ra, sa = P.render(final_scene, cam, 160, 90, 8, cull=True)
-    b, rb, sb = P.render(final_scene, cam, 160, 90, 8, cull=False)
+    a, ra, sa = P.render(final_scene, cam, 160, 90, 8, cull=True, cull_stats=True)
+    b, rb, sb = P.render(final_scene, cam, 160, 90, 8, cull=False, cull_stats=True)
     assert np.array_equal(bits(a), bits(b)) and np.array_equal(ra, rb)
     assert sa["rays"] == sb["rays"]
     assert sa["tests_executed"] < sb["tests_executed"] / 5, (sa, sb)
+    # the default (non-counting) kernel: same bits and rays, no test counts
+    c, rc, sc = P.render(final_scene, cam, 160, 90, 8)
+    assert np.array_equal(bits(a), bits(c)) and np.array_equal(ra, rc)
+    assert (sc["rays"], sc["rays_traced"]) == (sa["rays"], sa["rays_traced"])
+    assert sc["tests_executed"] == 0 and sc["box_tests"] == 0, sc
     want, _, rays = oracle_mod.render(final_scene, cam, 160, 90, 8, threads=8)
     assert np.array_equal(bits(a), bits(want)) and sa["rays"] == rays
 
@@ -233,8 +238,8 @@ def test_trapped_termination_is_bit_identical(oracle_mod, final_scene):
     """ending paths stuck at an exact C == 0 fixed point changes no
     bit and no ray count; it removes most executed work on the final scene."""
     cam = P.camera_look_at(aspect=160 / 90)
-    a, ra, sa = P.render(final_scene, cam, 160, 90, 8, fixpoint=True)
-    b, rb, sb = P.render(final_scene, cam, 160, 90, 8, fixpoint=False)
+    a, ra, sa = P.render(final_scene, cam, 160, 90, 8, fixpoint=True, cull_stats=True)
+    b, rb, sb = P.render(final_scene, cam, 160, 90, 8, fixpoint=False, cull_stats=True)
     assert np.array_equal(bits(a), bits(b)) and np.array_equal(ra, rb)
     assert sa["rays"] == sb["rays"]
     assert sa["tests_executed"] < sb["tests_executed"] / 2, (sa, sb)

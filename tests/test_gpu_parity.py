@@ -294,7 +294,7 @@ def test_context_repeat_renders_stats(oracle_mod, monkeypatch):
     renders, RT_FLAG_NO_TAIL_PRIORITY and a multi-chunk render all give the
     same bits and the same statistics."""
     import torch
-    from petershirleyraytracer_amd.render import FLAG_NO_TAIL_PRIORITY
+    from petershirleyraytracer_amd.render import FLAG_CULL_STATS, FLAG_NO_TAIL_PRIORITY
     sph = oracle_mod.scene_random_spheres(1)
     cam = oracle_mod.camera_look_at(aspect=120 / 80)
     ctx = P.Context(0)
@@ -304,7 +304,8 @@ def test_context_repeat_renders_stats(oracle_mod, monkeypatch):
     s = ctx.stream()
     keys = ("rays", "tests_executed", "box_tests", "rays_traced")
     runs = []
-    for flags, buf_mb in ((0, None), (0, None), (FLAG_NO_TAIL_PRIORITY, None), (0, "1")):
+    C = FLAG_CULL_STATS
+    for flags, buf_mb in ((C, None), (C, None), (C | FLAG_NO_TAIL_PRIORITY, None), (C, "1")):
         if buf_mb:
             monkeypatch.setenv("PSRT_SAMPLE_BUF_MB", buf_mb)  # 9600 px x 10 B: 8-sample chunks
         ctx.render_device(P.params(120, 80, 300, flags=flags), acc.data_ptr(), rgb.data_ptr(), s)
