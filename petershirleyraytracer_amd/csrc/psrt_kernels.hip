@@ -1285,7 +1285,8 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       if (a.max_depth < 0) {  // main.cc:36-37 at the first call: black, no trace
         finish = true;
       } else {
-        ++rays;
+        // this ray is one of the reference's rays: counted in `traced` above
+        // (wave-uniform), added to the ray total at exit
         clk.util(kUHit);
         if constexpr (kBVH) {
           bool trapped;
@@ -1533,7 +1534,10 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
 #endif
   unsigned long long* const ctr = a.ray_counter + kShardStride * (blockIdx.x % kQueues);
   flush_counters(ctr, rays, cs.spheres, cs.boxes, lane);
-  if (lane == 0 && traced) atomicAdd(ctr + 3, traced);
+  if (lane == 0 && traced) {
+    atomicAdd(ctr, traced);      // the traced rays (the lanes' counters hold the trapped rest)
+    atomicAdd(ctr + 3, traced);  // rays_traced
+  }
   __syncthreads();  // every wave of the block has left the loop (and flushed to LDS)
   if (threadIdx.x < 3 && s_flush[threadIdx.x]) atomicAdd(ctr + threadIdx.x, s_flush[threadIdx.x]);
 }
