@@ -1041,7 +1041,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   uint64_t rng = 0;
   unsigned q = 0;     // pixel index within the shard
   unsigned su = 0;    // this sample's unit (q * s_count + sample index in the chunk)
-  unsigned rays = 0;
+  unsigned rays = 0;  // the reference rays of this lane's trapped paths (§9); traced ones: `traced`
   int hint = -1;  // sphere the ray starts on (the previous hit), tested first
   bool pending = false;  // parked for the next batched BVH pass
   unsigned wbox0 = 0;    // diagnostic build: box tests before this ray's walk
