@@ -12,11 +12,22 @@ color.h:8-24, per pixel); the uint8 rows are gathered to rank 0 over RCCL
 one JSON line; value = W*H*spp*K / wall, wall = max over ranks between
 barriers.
 
-Scaling (--scaling): "weak" (default) keeps each GPU's work fixed: on N GPUs
-the frame is the configured W x H at N x spp, rows interleaved, so every rank
-renders the configured frame's sample count (C3: 96 M samples per GPU; the
-8-GPU frame is 1200x800 at 800 spp). "strong" renders the configured frame
-itself on any N.
+Scaling (--scaling): "strong" (default) renders the configured frame itself
+on any N, rows interleaved over the ranks: the BASELINE metric (W*H*spp/wall
+at 1/2/4/8 GPUs) on one fixed workload. "weak" is an opt-in study that keeps
+each GPU's work fixed: on N GPUs the frame is the configured W x H at N x spp
+(config_id gets a "-weak" suffix, so its value is never read as the
+configured frame's number).
+
+The BASELINE's 8-GPU configuration (C4, 3840x2160x500) is
+    torchrun --nproc-per-node 8 bench.py --gpus 8 --config c4
+(strong, the default); the N=1 default stays C3 so BENCH and SCALE agree.
+
+Each timed step ends with the frame's write_color bytes in pinned host memory
+(a device-to-host copy of the rank-0 frame, main.cc:70,86: the reference's
+loop ends by emitting the image). After the timed steps, N > 1 renders one
+untimed frame, gathers its FP64 accumulators to rank 0 and compares sampled
+rows bit for bit with the reference itself (oracle/_ref/ref_render).
 
 Default workload (BASELINE.json north star, configs[2]): the final
 random-spheres scene (485 spheres), 1200x800, 100 spp, depth 50.
@@ -82,7 +93,9 @@ def parse():
     ap.add_argument("--max-depth", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target CPU work of the bounded reference baseline sample")
-    ap.add_argument("--cpu-procs", type=int, default=16)
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="reference processes of the CPU baseline (0 = every core this "
+                         "process may use: affinity mask, capped by the cgroup CPU quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--save-ppm", default="")
     ap.add_argument("--no-cull", action="store_true", help="force the linear sphere sweep")
@@ -96,9 +109,9 @@ def parse():
                          "0 = auto: 1 for multi-chunk frames, else 3)")
     ap.add_argument("--gate", action="store_true",
                     help="with --pipeline >= 3: frame k's trace waits on the device for frame k-2")
-    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
-                    help="weak: N GPUs render the frame at N x spp (per-GPU work fixed); "
-                         "strong: the configured frame on any N")
+    ap.add_argument("--scaling", default="strong", choices=("weak", "strong"),
+                    help="strong (default): the configured frame on any N; weak (study): "
+                         "N GPUs render the frame at N x spp (per-GPU work fixed)")
     ap.add_argument("--emulate-shard", default="",
                     help="R/G: one process renders only rank R's rows of a G-GPU run "
                          "(per-rank step time of the multi-GPU bench, on one GPU; "
@@ -113,16 +126,87 @@ def scene_of(cfg):
     return P.scene_random_spheres(1), P.camera_look_at(aspect=cfg["width"] / cfg["height"])
 
 
+def host_cpus():
+    """The host cores this process may use: the affinity mask, capped by the
+    cgroup v2 CPU quota (a GPU box's share of its host); plus nproc and the
+    CPU model for the record."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    return dict(nproc=os.cpu_count(), affinity=aff, cgroup_quota=quota, usable=usable,
+                cpu_model=model)
+
+
+def run_reference_rows(O, cfg, args, spp, row0, stride, rows, procs, td, tag=""):
+    """oracle/_ref/ref_render on `rows` rows (row0, row0 + stride, ...) at `spp`,
+    columns split over `procs` single-thread processes. Returns (wall seconds,
+    [(c0, c1, accum[rows, c1 - c0, 3])]) or None on failure."""
+    w, h = cfg["width"], cfg["height"]
+    cols = np.linspace(0, w, procs + 1).astype(int)
+    cmds = []
+    for p in range(procs):
+        if cols[p + 1] <= cols[p]:
+            continue
+        out = os.path.join(td, f"a{tag}{p}.bin")
+        cmds.append((cols[p], cols[p + 1], out,
+                     [O.REF_BIN, "--scene", cfg["scene"], "--width", str(w), "--height", str(h),
+                      "--spp", str(spp), "--depth", str(args.max_depth), "--seed", str(args.seed),
+                      "--rows", f"{row0}:{stride}:{rows}", "--cols", f"{cols[p]}:{cols[p + 1]}",
+                      "--accum", out]))
+    t0 = time.perf_counter()
+    running = [subprocess.Popen(c[3], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+               for c in cmds]
+    ok = all(pr.wait() == 0 for pr in running)
+    wall = time.perf_counter() - t0
+    if not ok:
+        return None
+    parts = [(c0, c1, np.fromfile(out, dtype=np.float64).reshape(rows, c1 - c0, 3))
+             for c0, c1, out, _ in cmds]
+    return wall, parts
+
+
+def compare_rows(O, parts, frame_acc, row0, stride, rows, spp):
+    """Bit-for-bit comparison of reference pixels with the GPU frame's."""
+    equal, n_pix, sq = True, 0, 0.0
+    sel = frame_acc[row0::stride][:rows]
+    for c0, c1, a in parts:
+        g = np.ascontiguousarray(sel[:, c0:c1])
+        equal &= bool(np.array_equal(a.view(np.uint64), g.view(np.uint64)))
+        n_pix += a.shape[0] * a.shape[1]
+        d = O.quantize(a, spp).astype(np.float64) - O.quantize(g, spp)
+        sq += float(np.sum(d * d))
+    mse = sq / max(1, 3 * n_pix)
+    psnr = "inf" if mse == 0 else round(10 * math.log10(255.0 ** 2 / mse), 3)
+    return dict(pixels_compared=n_pix, fp64_bit_identical=equal, ppm_psnr_db=psnr)
+
+
 def cpu_baseline(cfg, args, frame_acc):
     """The reference itself (oracle/_ref/ref_render: the reference sources
     compiled unmodified) on a bounded sample of the same workload: a set of
-    rows spread over the frame, columns split over worker processes. Also
-    checks those pixels against the GPU frame bit for bit."""
+    rows spread over the frame, columns split over one single-thread process
+    per usable host core; then one process alone on a smaller set of rows (the
+    1-thread rate). Also checks the sampled pixels against the GPU frame bit
+    for bit."""
     import oracle as O  # checker / baseline only
     if not O.have_ref():
         return None, None
     w, h, spp = cfg["width"], cfg["height"], cfg["spp"]
-    procs = max(1, min(args.cpu_procs, len(os.sched_getaffinity(0))))
+    hc = host_cpus()
+    procs = args.cpu_procs if args.cpu_procs > 0 else hc["usable"]
     # per-core reference rate (SURVEY.md §6): two-sphere 0.62 Ms/s, final 0.0232 Ms/s
     rate = 0.62e6 if cfg["scene"] == "two" else 0.0232e6
     want_samples = args.cpu_seconds * procs * rate
@@ -133,46 +217,64 @@ def cpu_baseline(cfg, args, frame_acc):
     rows = max(1, min(h, int(want_samples / (w * spp_eff))))
     stride = max(1, h // rows)
     rows = len(range(0, h, stride))
-    cols = np.linspace(0, w, procs + 1).astype(int)
     with tempfile.TemporaryDirectory() as td:
-        cmds = []
-        for p in range(procs):
-            if cols[p + 1] <= cols[p]:
-                continue
-            cmds.append((p, [O.REF_BIN, "--scene", cfg["scene"], "--width", str(w), "--height",
-                             str(h), "--spp", str(spp_eff), "--depth", str(args.max_depth),
-                             "--seed", str(args.seed), "--rows", f"0:{stride}:{rows}",
-                             "--cols", f"{cols[p]}:{cols[p + 1]}",
-                             "--accum", os.path.join(td, f"a{p}.bin")]))
-        t0 = time.perf_counter()
-        running = [(p, subprocess.Popen(c, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE))
-                   for p, c in cmds]
-        ok = all(pr.wait() == 0 for _, pr in running)
-        wall = time.perf_counter() - t0
-        if not ok:
+        r = run_reference_rows(O, cfg, args, spp_eff, 0, stride, rows, procs, td)
+        if r is None:
             return None, None
+        wall, parts = r
         samples = rows * w * spp_eff
-        parity = None
-        if frame_acc is not None and spp_eff == spp:
-            equal, n_pix, sq = True, 0, 0.0
-            for p, _ in cmds:
-                a = np.fromfile(os.path.join(td, f"a{p}.bin"), dtype=np.float64)
-                a = a.reshape(rows, cols[p + 1] - cols[p], 3)
-                g = np.ascontiguousarray(frame_acc[0:h:stride][:rows, cols[p]:cols[p + 1]])
-                equal &= bool(np.array_equal(a.view(np.uint64), g.view(np.uint64)))
-                n_pix += a.shape[0] * a.shape[1]
-                d = O.quantize(a, spp).astype(np.float64) - O.quantize(g, spp)
-                sq += float(np.sum(d * d))
-            mse = sq / max(1, 3 * n_pix)
-            psnr = "inf" if mse == 0 else round(10 * math.log10(255.0 ** 2 / mse), 3)
-            parity = dict(pixels_compared=n_pix, fp64_bit_identical=equal, ppm_psnr_db=psnr)
+        parity = compare_rows(O, parts, frame_acc, 0, stride, rows, spp) \
+            if frame_acc is not None and spp_eff == spp else None
+        # one process alone (1 thread), ~4 s of work: rows spread the same way
+        rows1 = max(1, int(4.0 * rate / (w * spp_eff)))
+        stride1 = max(1, h // rows1)
+        rows1 = len(range(stride1 // 2, h, stride1))
+        r1 = run_reference_rows(O, cfg, args, spp_eff, stride1 // 2, stride1, rows1, 1, td, "one")
+    one = None if r1 is None else rows1 * w * spp_eff / r1[0] / 1e6
     cb = dict(value=samples / wall / 1e6, unit="Msamples/s", cores=procs, kind="reference",
+              one_thread_value=one,
               per_process_value=samples / wall / 1e6 / procs,  # one core's share (1 thread each)
+              nproc=hc["nproc"], affinity_cpus=hc["affinity"], cgroup_cpu_quota=hc["cgroup_quota"],
+              cpu_model=hc["cpu_model"],
               sample=(f"{rows} rows (every {stride}th) x {w} cols x {spp_eff} spp "
                       f"= {samples} samples of the same workload; reference sources "
-                      f"(g++ -O2, unmodified) in {procs} single-thread processes, "
-                      f"{wall:.1f} s wall"))
+                      f"(g++ -O2, unmodified) in {procs} single-thread processes "
+                      f"(one per usable core: affinity {hc['affinity']}, cgroup quota "
+                      f"{hc['cgroup_quota']}), {wall:.1f} s wall; one_thread_value: "
+                      f"{rows1} rows x {w} x {spp_eff} spp in one process"
+                      + (f", {r1[0]:.1f} s" if r1 else "")))
     return cb, parity
+
+
+def verify_gathered(cfg, args, frame_acc, world):
+    """N > 1: compare sampled rows of the gathered FP64 frame with the
+    reference (every rank's rows are covered: the row stride is odd, so the
+    sampled rows run through every residue mod world)."""
+    import oracle as O  # checker only
+    if not O.have_ref():
+        return dict(checked=False, reason="oracle/_ref/ref_render absent")
+    w, h, spp = cfg["width"], cfg["height"], cfg["spp"]
+    if frame_acc.shape[0] != h or spp > 100:
+        return dict(checked=False, reason="weak-scaled or >100 spp frame")
+    procs = host_cpus()["usable"]
+    rate = 0.62e6 if cfg["scene"] == "two" else 0.0232e6
+    rows = max(world, min(h, int(6.0 * procs * rate / (w * spp))))
+    stride = max(1, h // rows) | 1
+    rows = len(range(0, h, stride))
+    with tempfile.TemporaryDirectory() as td:
+        r = run_reference_rows(O, cfg, args, spp, 0, stride, rows, procs, td)
+    if r is None:
+        return dict(checked=False, reason="reference run failed")
+    out = compare_rows(O, r[1], frame_acc, 0, stride, rows, spp)
+    out.update(checked=True, rows=f"0::{stride} ({rows} rows)",
+               ranks_covered=len({(k * stride) % world for k in range(rows)}),
+               gather="RCCL FP64 accumulators" if dist_backend() == "nccl" else dist_backend())
+    return out
+
+
+def dist_backend():
+    import torch.distributed as dist
+    return dist.get_backend() if dist.is_initialized() else "none"
 
 
 def profile_counters(config: str):
@@ -192,7 +294,10 @@ def profile_counters(config: str):
     try:
         c = d["counters"]
         cycles = c["GRBM_GUI_ACTIVE"] / 8
-        valu = dict(insts_per_launch=c["SQ_INSTS_VALU"], kernel_cycles=cycles,
+        valu = dict(kernel=d.get("kernel"), insts_per_launch=c["SQ_INSTS_VALU"],
+                    salu_insts_per_launch=c.get("SQ_INSTS_SALU"),
+                    branch_insts_per_launch=c.get("SQ_INSTS_BRANCH"),
+                    kernel_cycles=cycles,
                     simd_cycles_per_valu_inst=round(cycles * 1024 / c["SQ_INSTS_VALU"], 3),
                     note="a wave64 FP64 VALU op holds a SIMD 4 cycles (16 lanes/cycle)",
                     source=f"profiles/pmc_{config}.json")
@@ -234,10 +339,13 @@ def main():
 
     w, h, spp = cfg["width"], cfg["height"], cfg["spp"]
     spheres, cam = scene_of(cfg)
+    config_id = args.config
     # weak scaling: N GPUs (or an emulated shard of G) render N x spp
     n_shards = int(args.emulate_shard.split("/")[1]) if args.emulate_shard else world
     if args.scaling == "weak":
         spp *= n_shards
+        if n_shards > 1:
+            config_id = f"{args.config}-weak"  # not the configured frame: never read as its number
     # Frames in flight: each slot has its own context (work queue, sample
     # buffer, stats), stream and output rows, so frame k+1 fills the CUs that
     # frame k's last waves release (DESIGN.md §7 "Frame pipelining").
@@ -278,14 +386,22 @@ def main():
         candidates = [(1, True, False), (2, True, False), (3, True, False)]
     depth = max(c[0] for c in candidates)  # contexts / buffers to allocate
     ctxs = []
+    scene_ms = []  # rt_context_set_scene: host BVH / grid / neighbour lists + uploads
     for _ in range(depth):
         c = P.Context(local)
+        t0 = time.perf_counter()
         c.set_scene(spheres, cam)
+        scene_ms.append((time.perf_counter() - t0) * 1e3)
         ctxs.append(c)
     dev = torch.device("cuda", local)
     acc = [torch.zeros((rows, w, 3), dtype=torch.float64, device=dev) for _ in range(depth)]
     rgb = torch.zeros((h, w, 3), dtype=torch.uint8, device=dev) if rank == 0 and world > 1 else None
     rgb_rows = [torch.zeros((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(depth)]
+    # every step ends with the frame's bytes in pinned host memory (rank 0):
+    # one buffer per frame slot, so frames in flight never share one
+    host_rows = h if world > 1 else rows
+    host_rgb = [torch.empty((host_rows, w, 3), dtype=torch.uint8, pin_memory=True)
+                for _ in range(depth)] if rank == 0 else None
     # each frame slot renders on its context's own stream
     streams = [torch.cuda.ExternalStream(c.stream(), device=dev) for c in ctxs]
     # N > 1: every gather goes on one stream, in frame order on every rank
@@ -309,6 +425,8 @@ def main():
             st.wait_event(done[(step - 2) % run["dn"]])
         if world == 1:
             ctx.render_device(run["prm"], acc[sl].data_ptr(), rgb_rows[sl].data_ptr(), st.cuda_stream)
+            with torch.cuda.stream(st):  # the frame to the host (main.cc:70,86 emit the image)
+                host_rgb[sl].copy_(rgb_rows[sl], non_blocking=True)
             done[sl].record(st)
             frame = acc[sl]
             pending[sl] = (step, None)
@@ -332,6 +450,7 @@ def main():
                                              comm.cuda_stream)
                 else:
                     rgb.copy_(frame)
+                host_rgb[sl].copy_(rgb, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(comm)
         pending[sl] = (step, ev)
@@ -377,6 +496,21 @@ def main():
             el = float(t.item())
         return el
 
+    # One-time costs outside the timed steps: set_scene (above) and the
+    # camera-ray candidate lists, built by a context's first render and
+    # cached (psrt_capi.hip): that render's non-trace device time minus a
+    # cached render's
+    def one(ctx, sl):
+        ctx.render_device(prm, acc[sl].data_ptr(), rgb_rows[sl].data_ptr(), streams[sl].cuda_stream)
+        return ctx.sync_stats()
+    first = one(ctxs[0], 0)
+    again = one(ctxs[0], 0)
+    camlist_ms = max(0.0, (first["total_ms"] - first["kernel_ms"])
+                     - (again["total_ms"] - again["kernel_ms"]))
+    for k in range(1, depth):
+        one(ctxs[k], k)
+    torch.cuda.synchronize(dev)
+
     # untimed tuning runs: every candidate (depth, tail priority) renders
     # full frames; the fastest (max over ranks) is the one timed below
     def cname(c):
@@ -420,6 +554,29 @@ def main():
     total_samples = (rows if args.emulate_shard else h) * w * spp * args.steps
     value = total_samples / elapsed / 1e6
 
+    # per-rank kernel time and HBM fraction (rank 0 reports them all)
+    my_kms = float(np.mean(kernel_ms)) if kernel_ms else 0.0
+    my_hbm = rows * w * spp * SAMPLE_RECORD_BYTES / (my_kms * 1e-3) / PEAK_HBM if my_kms else 0.0
+    per_rank = [dict(rank=0, rows=rows, kernel_ms=round(my_kms, 3), hbm_frac=round(my_hbm, 6))]
+    if distributed:
+        t = torch.tensor([float(rank), float(rows), my_kms, my_hbm], dtype=torch.float64,
+                         device=dev)
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        per_rank = [dict(rank=int(p[0]), rows=int(p[1]), kernel_ms=round(float(p[2]), 3),
+                         hbm_frac=round(float(p[3]), 6)) for p in (q.cpu() for q in parts)]
+
+    # N > 1 self-check: one untimed frame, its FP64 accumulators gathered to
+    # rank 0 over the same backend (RCCL), sampled rows compared bit for bit
+    # with the reference itself
+    gathered = None
+    if world > 1:
+        ctxs[0].render_device(prm, acc[0].data_ptr(), 0, streams[0].cuda_stream)
+        ctxs[0].sync_stats()
+        torch.cuda.synchronize(dev)
+        gathered = gather_frame(acc[0], h, rank, world)
+        torch.cuda.synchronize(dev)
+
     if rank == 0:
         n = len(spheres)
         avg_ms = float(np.mean(kernel_ms))
@@ -456,7 +613,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic (procedural scene: final random-spheres, glibc srand(1); counter RNG seed 0)",
             "config": {"workload": cfg["desc"] + (f"; {n_shards} GPUs at {n_shards} x spp (weak scaling: {cfg['spp']} spp of work per GPU)" if args.scaling == "weak" and n_shards > 1 else ""),
-                       "config_id": args.config, "width": w,
+                       "config_id": config_id, "width": w,
                        "height": h, "spp": spp, "max_depth": args.max_depth, "spheres": n,
                        "parallelism": (f"emulated shard {args.emulate_shard} (rows {off}::{stride})"
                                        if args.emulate_shard else f"interleaved rows x{world}") + ((", RCCL FP64 framebuffer gather" if args.gather_fp64 else ", per-rank write_color + RCCL uint8 gather") if world > 1 else "")},
@@ -500,6 +657,15 @@ def main():
             "depth_tuning_ms": {k: round(v, 3) for k, v in tuning.items()} or None,
             # the same frames rendered one at a time (each waits for the last)
             "unpipelined": unpiped,
+            "per_rank": per_rank,
+            "timed_step": ("render + write_color + " + ("RCCL uint8 gather + " if world > 1 and not args.gather_fp64 else "RCCL FP64 gather + psrt_quantize + " if world > 1 else "")
+                           + "D2H of the frame's bytes into pinned host memory (rank 0)"),
+            # one-time costs, outside the timed steps
+            "one_time_ms": {"set_scene": round(scene_ms[0], 3),
+                            "camera_lists": round(camlist_ms, 3),
+                            "note": "set_scene: host BVH / grid / neighbour lists + uploads "
+                                    "(wall); camera_lists: psrt_camera_lists, first render's "
+                                    "non-trace device time minus a cached render's"},
         }
         if args.save_ppm and rgb is not None:
             P.write_ppm(args.save_ppm, rgb.cpu().numpy(), binary=True)
@@ -509,6 +675,11 @@ def main():
                 cb, parity = cpu_baseline(cfg, args, frame.cpu().numpy())
             except Exception as e:  # baseline is reported, never the target
                 print(f"cpu baseline failed: {e}", file=sys.stderr)
+        if world > 1:
+            try:
+                parity = verify_gathered(cfg, args, gathered.cpu().numpy(), world)
+            except Exception as e:  # reported, never the target
+                parity = dict(checked=False, reason=f"{type(e).__name__}: {e}")
         out["cpu_baseline"] = cb
         out["parity_vs_cpu"] = parity
         print(json.dumps(out), flush=True)

@@ -160,7 +160,10 @@ int rt_render_device(rt_context* ctx, const rt_params* params, double* d_accum,
  * gives each frame its own stream (bench.py frame pipelining). */
 void* rt_context_stream(rt_context* ctx);
 
-/* Wait for the context's last render and fill stats (counters + kernel_ms). */
+/* Wait for the context's last render and fill stats (counters + kernel_ms).
+ * Before the context's first render it fills zero counters and returns RT_OK.
+ * After a render that failed part-way it waits for the part that was enqueued;
+ * its counters are then not meaningful. */
 int rt_context_sync_stats(rt_context* ctx, rt_stats* stats);
 
 /* Device-side write_color over d_accum (rows*width*3) -> d_rgb8. */
@@ -232,8 +235,9 @@ int rt_debug_world_hit(const rt_sphere* spheres, int n_spheres, const double* ra
 
 /* Debug: as rt_debug_world_hit, with hints[k] (NULL = none; -1 = none for ray
  * k) naming the sphere ray k starts on. The trace kernel tests a bounce ray's
- * previous hit first and, from it, picks the neighbour list or direction map
- * (DESIGN.md §11, §12); the record is the reference's whatever the hint. */
+ * previous hit first and, when that hit is close to the ray's origin, takes
+ * that sphere's neighbour list as hit_quick's candidate list;
+ * the record is the reference's whatever the hint. */
 int rt_debug_world_hit_hint(const rt_sphere* spheres, int n_spheres, const double* rays,
                             const int* hints, int count, double* out, int cull);
 

@@ -148,6 +148,9 @@ struct rt_context {
   // on another stream waits for ev_all1 on the device, and host-side writes
   // (set_scene, reallocation) wait for it on the host (quiesce).
   bool in_flight = false;
+  // a render failed after its first trace launch: queue heads / counter sets
+  // may be non-zero until the next render re-zeroes them (stream-ordered)
+  bool dirty = false;
   rt_stats last{};
   int n_last = 0;
 };
@@ -182,6 +185,23 @@ int ensure_buf(rt_context* c, double** p, size_t* cap, size_t need) {
   *cap = need;
   return RT_OK;
 }
+
+// Scratch device allocation of a debug entry: freed on every return path,
+// after the context's stream (which may still read it) has drained.
+struct ScratchBuf {
+  void* p = nullptr;
+  hipStream_t st = nullptr;
+  explicit ScratchBuf(hipStream_t s) : st(s) {}
+  ScratchBuf(const ScratchBuf&) = delete;
+  ScratchBuf& operator=(const ScratchBuf&) = delete;
+  ~ScratchBuf() {
+    if (!p) return;
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(p);
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
 
 std::mutex g_default_mu;
 rt_context* g_default[64] = {};
@@ -659,6 +679,11 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     c->plist_cap = P;
     c->plist_valid = false;
   }
+  if (c->dirty) {  // an earlier render failed part-way: heads and sets back to zero
+    HIP_TRY(hipMemsetAsync(c->d_counters + kHeads, 0,
+                           (kCounterWords - kHeads) * sizeof(unsigned long long), st));
+    c->dirty = false;
+  }
   HIP_TRY(hipEventRecord(c->ev_all0, st));
   const int key[4] = {p->width, p->height, p->row_offset, p->row_stride};
   if (camlist && c->plist_valid && std::equal(key, key + 4, c->plist_key)) {
@@ -691,6 +716,12 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     c->plist_valid = true;
     bv.plist = c->d_plist;
   }
+  // A HIP failure after the first trace launch would leave the queue heads and
+  // counter sets non-zero (only psrt_reduce re-zeroes them): the context is
+  // marked dirty, the enqueued part is fenced by ev_all1 like a whole render,
+  // and the next render re-zeroes them with a stream-ordered memset first.
+  c->dirty = true;
+  auto enqueue_chunks = [&]() -> int {
   for (int ch = 0; ch < nchunks; ++ch) {
     const int s0 = (int)(ch * s_chunk);
     const int sc = (int)std::min<size_t>(s_chunk, (size_t)(p->spp - s0));
@@ -763,9 +794,16 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     hipLaunchKernelGGL(psrt::psrt_reduce, dim3(blocks), dim3(psrt::kReduceBlock), 0, st, ra);
     HIP_TRY(hipGetLastError());
   }
-  HIP_TRY(hipEventRecord(c->ev_all1, st));
-  c->in_flight = true;
+  return RT_OK;
+  };
+  rc = enqueue_chunks();
+  const hipError_t fence = hipEventRecord(c->ev_all1, st);
+  c->in_flight = fence == hipSuccess;
   c->last_stream = st;
+  if (rc) return rc;
+  if (fence != hipSuccess)
+    return set_error(RT_E_HIP, "hipEventRecord: %s", hipGetErrorString(fence));
+  c->dirty = false;
   c->ev_used = nchunks;
   c->last = rt_stats{};
   c->last.samples = (uint64_t)P * p->spp;
@@ -777,7 +815,10 @@ void* rt_context_stream(rt_context* c) { return c ? (void*)c->stream : nullptr; 
 
 int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   if (!c) return set_error(RT_E_INVALID, "rt_context_sync_stats: ctx is NULL");
-  if (!c->in_flight) return set_error(RT_E_INVALID, "rt_context_sync_stats: no render enqueued");
+  if (!c->in_flight) {  // nothing rendered yet: zero counters (ABI 2 behaviour)
+    if (s) *s = rt_stats{};
+    return RT_OK;
+  }
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipEventSynchronize(c->ev_all1));
   if ((PSRT_BLOCK_DONE & 4) && !(PSRT_BLOCK_DONE & 8) && c->d_block_done) {
@@ -951,22 +992,19 @@ int rt_debug_probe_f64(int op, const double* x, const double* y, double* out, in
   std::unique_lock<std::mutex> lk;
   int rc = get_default_context(&c, &lk);
   if (rc) return rc;
-  double *dx, *dy, *dout;
-  HIP_TRY(hipMalloc(&dx, n * sizeof(double)));
-  HIP_TRY(hipMalloc(&dy, n * sizeof(double)));
-  HIP_TRY(hipMalloc(&dout, n * sizeof(double)));
+  ScratchBuf dx(c->stream), dy(c->stream), dout(c->stream);
+  HIP_TRY(hipMalloc(&dx.p, n * sizeof(double)));
+  HIP_TRY(hipMalloc(&dy.p, n * sizeof(double)));
+  HIP_TRY(hipMalloc(&dout.p, n * sizeof(double)));
   // every copy on the context's stream: it is non-blocking, so null-stream
   // copies and memsets would not be ordered before the launch
-  HIP_TRY(hipMemcpyAsync(dx, x, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemcpyAsync(dy, y, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(dx.p, x, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(dy.p, y, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
   hipLaunchKernelGGL(psrt::psrt_probe_f64, dim3((n + 255) / 256), dim3(256), 0, c->stream, op,
-                     (const double*)dx, (const double*)dy, dout, (unsigned)n);
+                     dx.as<const double>(), dy.as<const double>(), dout.as<double>(), (unsigned)n);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(out, dout, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(out, dout.p, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  (void)hipFree(dx);
-  (void)hipFree(dy);
-  (void)hipFree(dout);
   return RT_OK;
 }
 
@@ -986,31 +1024,28 @@ int rt_debug_world_hit_hint(const rt_sphere* sph, int n, const double* rays, con
   rt_camera cam{};
   rc = rt_context_set_scene(c, sph, n, &cam);
   if (rc) return rc;
-  double *dr, *dout;
-  int* dh = nullptr;
-  HIP_TRY(hipMalloc(&dr, (size_t)count * 8 * sizeof(double)));
-  HIP_TRY(hipMalloc(&dout, (size_t)count * 9 * sizeof(double)));
+  ScratchBuf dr(c->stream), dout(c->stream), dh(c->stream);
+  HIP_TRY(hipMalloc(&dr.p, (size_t)count * 8 * sizeof(double)));
+  HIP_TRY(hipMalloc(&dout.p, (size_t)count * 9 * sizeof(double)));
   // every copy and the memset on the context's stream: it is non-blocking, so
   // null-stream work would not be ordered before the launch (a null-stream
   // memset of dout once raced with the kernel and zeroed part of its output)
-  HIP_TRY(hipMemcpyAsync(dr, rays, (size_t)count * 8 * sizeof(double), hipMemcpyHostToDevice,
+  HIP_TRY(hipMemcpyAsync(dr.p, rays, (size_t)count * 8 * sizeof(double), hipMemcpyHostToDevice,
                          c->stream));
-  HIP_TRY(hipMemsetAsync(dout, 0, (size_t)count * 9 * sizeof(double), c->stream));
+  HIP_TRY(hipMemsetAsync(dout.p, 0, (size_t)count * 9 * sizeof(double), c->stream));
   if (hints) {
-    HIP_TRY(hipMalloc(&dh, (size_t)count * sizeof(int)));
-    HIP_TRY(hipMemcpyAsync(dh, hints, (size_t)count * sizeof(int), hipMemcpyHostToDevice,
+    HIP_TRY(hipMalloc(&dh.p, (size_t)count * sizeof(int)));
+    HIP_TRY(hipMemcpyAsync(dh.p, hints, (size_t)count * sizeof(int), hipMemcpyHostToDevice,
                            c->stream));
   }
   hipLaunchKernelGGL(psrt::psrt_probe_hit, dim3((count + 63) / 64), dim3(64), 0, c->stream,
-                     (const double4*)c->d_geo, (const double*)c->d_inv_r, n, (const double*)dr,
-                     (const int*)dh, dout, (unsigned)count, bvh_view(c), (cull && c->bvh) ? 1 : 0);
+                     (const double4*)c->d_geo, (const double*)c->d_inv_r, n, dr.as<const double>(),
+                     dh.as<const int>(), dout.as<double>(), (unsigned)count, bvh_view(c),
+                     (cull && c->bvh) ? 1 : 0);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(out, dout, (size_t)count * 9 * sizeof(double), hipMemcpyDeviceToHost,
+  HIP_TRY(hipMemcpyAsync(out, dout.p, (size_t)count * 9 * sizeof(double), hipMemcpyDeviceToHost,
                          c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  (void)hipFree(dr);
-  (void)hipFree(dout);
-  (void)hipFree(dh);
   return RT_OK;
 }
 

@@ -5,7 +5,8 @@
 Writes <dst>/kernel_stats_<cfg>.csv (the --stats summary as produced),
 <dst>/pmc_<cfg>.csv (per-dispatch counters of the psrt kernels) and
 profiles/pmc_<cfg>.json (per-launch HBM bytes + derived rates that bench.py
-reads for roofline.traffic). gfx950 corrections (MI355X_MICROARCH.md §HBM):
+reads for roofline.traffic). Only the timed kernel variant (TIMED below)
+enters the summary: counters, kernel_stats and dispatch durations alike. gfx950 corrections (MI355X_MICROARCH.md §HBM):
 FETCH_SIZE counts half the bytes of wide coalesced reads -> doubled; counters
 are in KiB; GRBM_GUI_ACTIVE sums the 8 XCDs.
 """
@@ -20,6 +21,17 @@ src, dst, cfg = sys.argv[1], sys.argv[2], sys.argv[3]
 os.makedirs(dst, exist_ok=True)
 stats = os.path.join(src, "trace", "run_kernel_stats.csv")
 shutil.copy(stats, os.path.join(dst, f"kernel_stats_{cfg}.csv"))
+# The timed kernel of bench.py is the default (non-counting) variant
+# psrt_trace<kBVH, kStamps, kLds, kCount> = <true, false, true, false>; the
+# bench also runs one untimed RT_FLAG_CULL_STATS frame (<..., true>), whose
+# counters, duration and kernel_stats row must not stand for the timed one.
+TIMED = os.environ.get("PSRT_TIMED_KERNEL", "psrt_trace<true, false, true, false>")
+
+
+def is_timed(name):
+    return TIMED in name
+
+
 rows = []
 for f in sorted(glob.glob(os.path.join(src, "pmc_*", "run_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
@@ -32,22 +44,25 @@ with open(os.path.join(dst, f"pmc_{cfg}.csv"), "w", newline="") as f:
     w.writeheader()
     for r in rows:
         w.writerow({k: r[k] for k in keys})
-c = {}
+# per counter: the mean over the timed kernel's dispatches (one per PMC pass
+# and timed frame; the counting frame's dispatches are left out)
+vals = {}
 for r in rows:
-    if "psrt_trace" in r["Kernel_Name"]:
-        c[r["Counter_Name"]] = float(r["Counter_Value"])
-        c.setdefault("_dur_ns", []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-dur = sorted(c.pop("_dur_ns"))[len(c.get("_dur_ns", [])) // 2] if "_dur_ns" in c else None
+    if is_timed(r["Kernel_Name"]):
+        vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+c = {k: sum(v) / len(v) for k, v in vals.items()}
+dispatches = {k: len(v) for k, v in vals.items()}
 avg = {}
 for line in csv.DictReader(open(stats)):
-    if "psrt_trace" in line["Name"]:
-        avg = dict(calls=int(line["Calls"]), average_ns=float(line["AverageNs"]))
+    if is_timed(line["Name"]):
+        avg = dict(kernel=line["Name"][:80], calls=int(line["Calls"]),
+                   average_ns=float(line["AverageNs"]))
 # per-dispatch durations: the first launch is bench.py's warmup step, which
 # bench.py's own HIP-event average leaves out; report the timed launches too
 trace = os.path.join(src, "trace", "run_kernel_trace.csv")
 if os.path.exists(trace):
     d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-         for r in csv.DictReader(open(trace)) if "psrt_trace" in r["Kernel_Name"]]
+         for r in csv.DictReader(open(trace)) if is_timed(r["Kernel_Name"])]
     if len(d) > 1:
         avg["average_ns_after_warmup"] = sum(d[1:]) / len(d[1:])
     # bench.py renders its timed frames pipelined (a dispatch's span then
@@ -61,7 +76,7 @@ fetch = c.get("FETCH_SIZE", 0.0) * 1024 * 2
 write = c.get("WRITE_SIZE", 0.0) * 1024
 secs = avg.get("average_ns_unpipelined", avg.get("average_ns", 0)) * 1e-9
 out = {
-    "kernel": "psrt_trace", "config": cfg, "kernel_stats": avg,
+    "kernel": TIMED, "config": cfg, "kernel_stats": avg, "pmc_dispatches": dispatches,
     "hbm_bytes_per_launch": fetch + write,
     "fetch_bytes_per_launch_x2": fetch, "write_bytes_per_launch": write,
     "hbm_gbps": (fetch + write) / secs / 1e9 if secs else None,
@@ -70,6 +85,11 @@ out = {
 }
 if "SQ_INSTS_VALU" in c and "SQ_WAVES" in c:
     out["valu_insts_per_wave"] = c["SQ_INSTS_VALU"] / c["SQ_WAVES"]
+if "GRBM_GUI_ACTIVE" in c:
+    cyc = c["GRBM_GUI_ACTIVE"] / 8  # one XCD's clock over the launch
+    for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_BRANCH"):
+        if k in c and c[k]:
+            out[f"simd_cycles_per_{k[9:].lower()}"] = cyc * 1024 / c[k]
 json.dump(out, open(os.path.join(ROOT := os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                  "profiles", f"pmc_{cfg}.json"), "w"), indent=1)
 json.dump(out, open(os.path.join(dst, f"pmc_{cfg}.json"), "w"), indent=1)

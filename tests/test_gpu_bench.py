@@ -1,0 +1,73 @@
+"""bench.py end to end on one GPU (BASELINE metric line).
+
+N = 1: the line carries the timed step's D2H, the one-time costs, the CPU
+baseline on the usable host cores with a 1-process rate, and the bit-for-bit
+parity of the baseline's pixels. N = 2: two ranks rehearsed on the one GPU
+over gloo (RCCL refuses two ranks on one device; the 8-GPU RCCL run is the
+driver's) render the strong-scaled frame, and the gathered FP64 frame's
+sampled rows match the reference itself (oracle/_ref/ref_render) bit for bit,
+rows of both ranks included.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _last_json(out: str) -> dict:
+    lines = [l for l in out.splitlines() if l.startswith("{") and '"metric"' in l]
+    assert lines, out[-2000:]
+    return json.loads(lines[-1])
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _have_ref() -> bool:
+    return os.path.exists(os.path.join(ROOT, "oracle", "_ref", "ref_render"))
+
+
+def test_bench_single_gpu_line():
+    r = subprocess.run([sys.executable, "bench.py", "--config", "c1", "--steps", "3", "--warmup",
+                        "1", "--cpu-seconds", "1"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 1 and d["scaling"] == "strong" and d["config"]["config_id"] == "c1"
+    assert "D2H" in d["timed_step"]
+    assert d["one_time_ms"]["set_scene"] >= 0 and d["one_time_ms"]["camera_lists"] >= 0
+    assert len(d["per_rank"]) == 1
+    if _have_ref():
+        cb = d["cpu_baseline"]
+        assert cb["kind"] == "reference" and cb["cores"] >= 1 and cb["one_thread_value"] > 0
+        assert "cpu_model" in cb and "nproc" in cb
+        assert d["parity_vs_cpu"]["fp64_bit_identical"] is True
+
+
+def test_bench_two_ranks_gathered_frame_matches_reference():
+    env = dict(os.environ, PSRT_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1",
+               OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+           "--gpus", "2", "--config", "c1", "--steps", "3", "--warmup", "1", "--pipeline", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["config"]["config_id"] == "c1"
+    assert sorted(p["rank"] for p in d["per_rank"]) == [0, 1]
+    assert sum(p["rows"] for p in d["per_rank"]) == 225
+    par = d["parity_vs_cpu"]
+    if not _have_ref():
+        assert par["checked"] is False
+        return
+    assert par["checked"] is True, par
+    assert par["fp64_bit_identical"] is True and par["ranks_covered"] == 2, par
