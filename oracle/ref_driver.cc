@@ -91,12 +91,55 @@ int run_kat(const std::string& path) {
   return 0;
 }
 
+// Known-answer mode over one scene: the first line of the file is
+// "n  cx cy cz r (n times)", every further line one ray "ox oy oz dx dy dz
+// tmin tmax" (hex floats); output as run_kat, one line per ray. For ray sets
+// too large to repeat the sphere list on every line (tests/golden/
+// make_culling_kat.py: tens of thousands of rays on the 485-sphere scene).
+int run_kat_scene(const std::string& path) {
+  std::ifstream in(path);
+  std::string line;
+  if (!std::getline(in, line)) return 2;
+  std::istringstream hs(line);
+  auto rdh = [&]() { std::string t; hs >> t; return std::strtod(t.c_str(), nullptr); };
+  const int n = (int)rdh();
+  hittable_list world;
+  std::vector<std::shared_ptr<sphere>> sp;
+  for (int k = 0; k < n; ++k) {
+    double cx = rdh(), cy = rdh(), cz = rdh(), r = rdh();
+    sp.push_back(make_shared<sphere>(point3(cx, cy, cz), r));
+    world.add(sp.back());
+  }
+  while (std::getline(in, line)) {
+    if (line.empty()) continue;
+    std::istringstream ss(line);
+    auto rd = [&]() { std::string t; ss >> t; return std::strtod(t.c_str(), nullptr); };
+    double ox = rd(), oy = rd(), oz = rd(), dx = rd(), dy = rd(), dz = rd();
+    double tmin = rd(), tmax = rd();
+    ray r(point3(ox, oy, oz), vec3(dx, dy, dz));
+    hit_record rec;
+    if (!world.hit(r, tmin, tmax, rec)) {
+      std::printf("-1\n");
+      continue;
+    }
+    int idx = -1;  // which object produced rec: replay the list scan (hittable_list.cc:9-17)
+    double closest = tmax;
+    hit_record tmp;
+    for (int k = 0; k < n; ++k)
+      if (sp[k]->hit(r, tmin, closest, tmp)) { closest = tmp.t; idx = k; }
+    std::printf("%d %a %a %a %a %a %a %a %d\n", idx, rec.p.x(), rec.p.y(), rec.p.z(),
+                rec.normal.x(), rec.normal.y(), rec.normal.z(), rec.t, (int)rec.front_face);
+  }
+  return 0;
+}
+
 void usage() {
   std::fprintf(stderr,
                "ref_render [--reference-main] [--width W] [--height H] [--spp S]\n"
                "  [--depth D] [--scene two|final] [--scene-seed N] [--rng glibc|counter]\n"
                "  [--seed N] [--rows OFF:STRIDE[:COUNT]] [--accum FILE] [--ppm FILE]\n"
-               "  [--dump-scene FILE] [--camera default|lookat] [--kat FILE] [--cols C0:C1]\n");
+               "  [--dump-scene FILE] [--camera default|lookat] [--kat FILE] [--kat-scene FILE]\n"
+               "  [--cols C0:C1]\n");
 }
 
 }  // namespace
@@ -106,7 +149,8 @@ int main(int argc, char** argv) {
   int col0 = 0, col1 = -1;  // --cols: render only columns [col0, col1) of each row
   unsigned scene_seed = 1;
   uint64_t seed = 0;
-  std::string scene = "two", rng = "counter", accum_path, ppm_path, dump_path, cam_kind, kat_path;
+  std::string scene = "two", rng = "counter", accum_path, ppm_path, dump_path, cam_kind, kat_path,
+      kat_scene_path;
   bool run_reference_main = false;
   for (int a = 1; a < argc; ++a) {
     std::string k = argv[a];
@@ -128,6 +172,7 @@ int main(int argc, char** argv) {
     else if (k == "--dump-scene") dump_path = next();
     else if (k == "--camera") cam_kind = next();
     else if (k == "--kat") kat_path = next();
+    else if (k == "--kat-scene") kat_scene_path = next();
     else if (k == "--cols") {
       std::string v = next();
       if (std::sscanf(v.c_str(), "%d:%d", &col0, &col1) != 2) { usage(); return 2; }
@@ -139,6 +184,7 @@ int main(int argc, char** argv) {
   }
   if (run_reference_main) return reference_main();
   if (!kat_path.empty()) return run_kat(kat_path);
+  if (!kat_scene_path.empty()) return run_kat_scene(kat_scene_path);
 
   // ---- world (main.cc:61-63, or the final scene) ----
   hittable_list world;

@@ -131,8 +131,6 @@ struct rt_context {
   // [8, 128) diagnostic stamps; queue heads at kHeads, statistics counter sets
   // (rays, sphere tests, box tests, traced rays) at kSets, kShardStride apart
   unsigned long long* d_counters = nullptr;
-  unsigned* d_block_done = nullptr;  // PSRT_BLOCK_DONE builds (zeroed once, self-resetting)
-  size_t block_done_cap = 0;
   // The render's statistics, written by its last psrt_reduce straight into
   // pinned host memory: reading them back needs no copy kernel, which (like
   // any kernel) would wait for a free CU slot behind the next frame's
@@ -299,7 +297,6 @@ int rt_context_destroy(rt_context* c) {
   (void)hipFree(c->d_plist);
   (void)hipFree(c->d_wave_log);
   (void)hipFree(c->d_counters);
-  if (c->d_block_done) (void)hipFree(c->d_block_done);
   (void)hipFree(c->d_nodes);
   (void)hipFree(c->d_leaf_geo);
   (void)hipFree(c->d_leaf_idx);
@@ -730,19 +727,6 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     ta.div_s = fast_div_make((unsigned)sc);
     ta.total_units = (uint64_t)P * sc;
     queue_phases(ta, use_bvh ? c->grid_bvh : c->grid, use_bvh);
-    ta.block_done = nullptr;
-    ta.block_units = 64u * (unsigned)sc;
-    if (PSRT_BLOCK_DONE) {
-      const size_t nb = (P + 63) / 64;
-      if (nb > c->block_done_cap) {
-        if (c->d_block_done) HIP_TRY(hipFree(c->d_block_done));
-        c->d_block_done = nullptr;
-        HIP_TRY(hipMalloc(&c->d_block_done, nb * sizeof(unsigned)));
-        HIP_TRY(hipMemsetAsync(c->d_block_done, 0, nb * sizeof(unsigned), st));
-        c->block_done_cap = nb;
-      }
-      ta.block_done = c->d_block_done;
-    }
     HIP_TRY(hipEventRecord(c->ev[2 * ch], st));
     const double4* g4 = c->d_geo;
     const double* ir = c->d_inv_r;
@@ -821,15 +805,6 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   }
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipEventSynchronize(c->ev_all1));
-  if ((PSRT_BLOCK_DONE & 4) && !(PSRT_BLOCK_DONE & 8) && c->d_block_done) {
-    // measurement builds: every block completed, so every counter is back at 0
-    std::vector<unsigned> bd(c->block_done_cap);
-    HIP_TRY(hipMemcpy(bd.data(), c->d_block_done, bd.size() * sizeof(unsigned),
-                      hipMemcpyDeviceToHost));
-    size_t bad = 0;
-    for (unsigned v : bd) bad += v != 0;
-    if (bad) std::fprintf(stderr, "psrt: %zu block counters not zero after a render\n", bad);
-  }
   // the render's last psrt_reduce wrote its totals into pinned host memory
   unsigned long long cnt[4];
   for (int k = 0; k < 4; ++k) cnt[k] = ((volatile unsigned long long*)c->h_stats)[k];

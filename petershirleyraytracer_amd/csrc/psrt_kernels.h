@@ -64,10 +64,6 @@ constexpr int kReduceBlock = 64;   // psrt_reduce: one wave per 64 pixels
 constexpr int kReduceTile = PSRT_REDUCE_TILE;  // samples per pixel per LDS tile: 16 or 32
 constexpr size_t kSampleBytes = sizeof(double) + sizeof(unsigned short);
 
-#ifndef PSRT_BLOCK_DONE
-#define PSRT_BLOCK_DONE 0  // measurement, bits: 1 sc1 record stores,
-                           // 2 wait for them, 4 per-block completion atomics
-#endif
 
 struct TraceArgs {
   int n;               // spheres (geo: {cx, cy, cz, r*r}, inv_r: 1.0/r)
@@ -100,9 +96,6 @@ struct TraceArgs {
   FastDiv div_s, div_w;             // unit / s_count, q / width
   unsigned flush_at;                // per-lane counters flush to the totals at this value
   int tail_prio;                    // raise the issue priority of waves whose queue is empty
-  unsigned* block_done;             // PSRT_BLOCK_DONE measurement builds: per 64-pixel block,
-                                    // records stored so far, else nullptr
-  unsigned block_units;             // units of a full 64-pixel block (64 * s_count)
 };
 
 // BVH node as the device reads it (two float4, from psrt_bvh.h BvhNode):

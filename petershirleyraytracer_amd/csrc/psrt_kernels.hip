@@ -28,50 +28,17 @@
 #include "psrt_device.h"
 #include "psrt_kernels.h"
 
-#ifndef PSRT_ABLATE
-#define PSRT_ABLATE 0  // measurement builds: 1 = hit_quick twice, 2 = two trials per trial,
-                       // 3 = the BVH walk twice; sub-sections of hit_quick twice: 4 = the hint
-                       // test, 5 = the big spheres, 6 = grid_locate, 7 = the candidate loop;
-                       // 8 = the refill's per-lane setup, 9 = the scatter
-#endif
-// Ablation: keep a measurement copy's results alive without storing them.
-#if PSRT_ABLATE
-#define PSRT_SINK(x) asm volatile("" ::"v"(x))
-#endif
-
-#ifndef PSRT_SLAB_PK
-#define PSRT_SLAB_PK 0  // 1: slab-test FMAs as packed FP32 pairs (-2% VALU, yet 1% slower)
-#endif
-
-#ifndef PSRT_SLAB_ASM
-#define PSRT_SLAB_ASM 1  // slab test min/max as inline asm (no per-box NaN canonicalisation)
-#endif
-
-#ifndef PSRT_WALK_PRIO
-#define PSRT_WALK_PRIO 3  // s_setprio of a wave during its batched BVH walk (0 = unchanged)
-#endif
-
-#ifndef PSRT_NT_STORE
-#define PSRT_NT_STORE 1  // sample records with non-temporal stores
-#endif
-
-#ifndef PSRT_HIT_PRIO
-#define PSRT_HIT_PRIO 2  // s_setprio of a wave during hit_quick (0 = unchanged)
-#endif
-
-#ifndef PSRT_REFILL_PRIO
-#define PSRT_REFILL_PRIO 0  // s_setprio of a wave in its refill block (0 = base)
-#endif
-
-#ifndef PSRT_SCATTER_PRIO
-#define PSRT_SCATTER_PRIO 0  // s_setprio of a wave in its scatter block (0 = base)
-#endif
-
-#ifndef PSRT_TAIL_PRIO
-#define PSRT_TAIL_PRIO 1  // s_setprio of a wave once the work queue is empty (0 = unchanged)
-#endif
-
 namespace psrt {
+
+// Wave issue priorities (s_setprio; DESIGN.md §4 "Issue priorities"): a wave
+// raises its priority during the latency-bound sections (the batched BVH
+// walk, hit_quick) and, once the work queue is empty, keeps a raised base
+// priority for the launch tail (TraceArgs::tail_prio).
+constexpr int kWalkPrio = 3;
+constexpr int kHitPrio = 2;
+constexpr int kTailPrio = 1;
+// Minimum waves per SIMD asked of the register allocator (80 VGPRs).
+constexpr int kTraceWaves = 6;
 
 __device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
 
@@ -180,9 +147,6 @@ __device__ __forceinline__ void sample_colour(double tt, unsigned short kk, doub
   }
 }
 
-#ifndef PSRT_FAST_SQRT
-#define PSRT_FAST_SQRT 1  // sqrt without the denormal scaling / class fixup where not needed
-#endif
 
 // sqrt (sphere.cc:19) as the compiler's correctly rounded f64 expansion
 // (v_rsq_f64, then Goldschmidt/Newton steps), minus its range handling: for
@@ -190,7 +154,6 @@ __device__ __forceinline__ void sample_colour(double tt, unsigned short kk, doub
 // fixup is not taken, so the steps below are exactly the ones it runs. Other
 // inputs (0, tiny, +inf, NaN) take __builtin_sqrt behind a wave-uniform branch.
 __device__ __forceinline__ double sqrt_f64(double x) {
-#if PSRT_FAST_SQRT
   const double r = __builtin_amdgcn_rsq(x);
   double g = x * r;
   double h = r * 0.5;
@@ -206,9 +169,6 @@ __device__ __forceinline__ double sqrt_f64(double x) {
     if (slow) g = __builtin_sqrt(x);
   }
   return g;
-#else
-  return __builtin_sqrt(x);
-#endif
 }
 
 // Root selection of sphere.cc:24-31 over [0, tmax], bit for bit, with one
@@ -334,9 +294,6 @@ __device__ __forceinline__ HitRec hit_record_of(const double4 s, double ir, doub
 // nearer the surface always take the full test.
 // Returns false when the pre-reject decided the sphere, true when the full
 // test ran. *c_out (if given) receives C = amc.amc - r^2 as sphere.cc:11 forms it.
-#ifndef PSRT_PRE2
-#define PSRT_PRE2 0  // 1: pre-reject as one comparison (max of the two bounds): measured +1% VALU
-#endif
 
 __device__ __forceinline__ bool test_sphere(const double4 s, int idx, double ox, double oy,
                                             double oz, double dx, double dy, double dz,
@@ -345,23 +302,11 @@ __device__ __forceinline__ bool test_sphere(const double4 s, int idx, double ox,
   const double ax = ox - s.x, ay = oy - s.y, az = oz - s.z;
   const double c = ((ax * ax + ay * ay) + az * az) - s.w;
   if (c_out) *c_out = c;
-#if PSRT_PRE2
-  // the same two conditions as one comparison, strict:
-  // C^2 > max(2^-34 (C + r^2), best_t^2 A (1 + 2^-4)) k2 (best_t = inf: never);
-  // k2 by one FMA (a bound of ours, not reference arithmetic: its rounding is
-  // ~2^-52, far inside the 2^-4 and 2^-33 margins)
-  if (c > 0.0) {
-    const double k2 = 2.0 * __builtin_fma(2.0, s.w, c);
-    const double m = __builtin_fmax(0x1p-34 * (c + s.w), (best_t * best_t) * A * (1.0 + 0x1p-4));
-    if (c * c > m * k2) return false;
-  }
-#else
   if (c > 0.0 && best_t < 1e100) {
     const double c2 = c * c, k2 = 2.0 * (c + 2.0 * s.w);
     if (c2 >= 0x1p-34 * (c + s.w) * k2 && (best_t * best_t) * A * k2 * (1.0 + 0x1p-4) < c2)
       return false;
   }
-#endif
   const double hb = (dx * ax + dy * ay) + dz * az;
   const double disc = hb * hb - A * c;
   if (disc < 0.0) return true;
@@ -415,9 +360,6 @@ __device__ __forceinline__ GridC grid_consts(const BvhView& bv) {
   return g;
 }
 
-#ifndef PSRT_GRID_INT
-#define PSRT_GRID_INT 1  // grid_locate on saturating floor-converts + integer clamps
-#endif
 
 // floor(x) as int, saturating (NaN -> 0): one v_cvt_flr_i32_f32
 __device__ __forceinline__ int cvt_flr_i32(float x) {
@@ -443,7 +385,6 @@ __device__ __forceinline__ int grid_locate(const GridC& bv, double ox, double oy
   const float tb = (float)bt * 1.00000048f;
   int ci[3];
   bool outside = false, ok = true, one = true;
-#if PSRT_GRID_INT
   // Cell range [c0, c1] of the widened segment per axis, from saturating
   // floor-converts (huge coordinates saturate, and the caller's range guard
   // keeps NaN out). Outside the grid when c1 < 0 or c0 > top on some axis:
@@ -463,25 +404,6 @@ __device__ __forceinline__ int grid_locate(const GridC& bv, double ox, double oy
     one = one && c1 == c0;
     ci[k] = c0;
   }
-#else
-  const float m = bv.gmargin;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const float e = __builtin_fmaf(tb, d3[k], o3[k]);
-    const float lo = fminf(o3[k], e) - m, hi = fmaxf(o3[k], e) + m;
-    const float glo = bv.glo[k], ghi = bv.ghi[k];
-    if (hi < glo || lo > ghi) outside = true;
-    // cell range of the widened segment, clipped to the grid (in float, before
-    // the conversion: huge or NaN coordinates clip too): a hit point lies in a
-    // padded sphere box, hence in a cell of the grid
-    const float top = (float)(bv.gdims[k] - 1);
-    const int c0 = (int)fminf(fmaxf(__builtin_floorf((lo - glo) * bv.ginv), 0.0f), top);
-    const int c1 = (int)fminf(fmaxf(__builtin_floorf((hi - glo) * bv.ginv), 0.0f), top);
-    ok = ok && c1 - c0 <= 1;
-    one = one && c1 == c0;
-    ci[k] = c0;
-  }
-#endif
   if (outside) return kGridOutside;
   if (!ok) return kGridNone;
   // one cell: its list; two cells on some axis: the 2x2x2 block list from ci
@@ -505,21 +427,9 @@ __device__ __forceinline__ float safe_inv(float d) {
 __device__ __forceinline__ bool slab_hit(const float4 n0, const float4 n1, float ix, float iy,
                                          float iz, float oix, float oiy, float oiz, float tlo,
                                          float tmax) {
-#if PSRT_SLAB_PK
-  // packed FP32 (v_pk_fma_f32, two FMAs per issue) on the node's coordinate
-  // pairs: (x0, y0), (x1, y1), (z0, z1)
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  const f2 ixy = {ix, iy}, oxy = {-oix, -oiy};
-  const f2 txy0 = __builtin_elementwise_fma((f2){n0.x, n0.y}, ixy, oxy);
-  const f2 txy1 = __builtin_elementwise_fma((f2){n0.z, n0.w}, ixy, oxy);
-  const f2 tz = __builtin_elementwise_fma((f2){n1.x, n1.y}, (f2){iz, iz}, (f2){-oiz, -oiz});
-  const float x0 = txy0.x, y0 = txy0.y, x1 = txy1.x, y1 = txy1.y, z0 = tz.x, z1 = tz.y;
-#else
   const float x0 = __builtin_fmaf(n0.x, ix, -oix), x1 = __builtin_fmaf(n0.z, ix, -oix);
   const float y0 = __builtin_fmaf(n0.y, iy, -oiy), y1 = __builtin_fmaf(n0.w, iy, -oiy);
   const float z0 = __builtin_fmaf(n1.x, iz, -oiz), z1 = __builtin_fmaf(n1.y, iz, -oiz);
-#endif
-#if PSRT_SLAB_ASM
   // v_min3/v_max3 directly: no NaN canonicalisation of tlo / tmax per box
   // (NaN cannot occur: finite boxes, safe_inv directions, finite tmax)
   float tn, tf, a, b;
@@ -533,10 +443,6 @@ __device__ __forceinline__ bool slab_hit(const float4 n0, const float4 n1, float
   asm("v_min3_f32 %0, %1, %2, %3" : "=v"(tf) : "v"(a), "v"(b), "v"(tmax));
   asm("v_max_f32 %0, %1, %2" : "=v"(a) : "v"(z0), "v"(z1));
   asm("v_min_f32 %0, %1, %2" : "=v"(tf) : "v"(tf), "v"(a));
-#else
-  const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tlo));
-  const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tmax));
-#endif
   return tn <= tf;
 }
 
@@ -613,15 +519,6 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     clk.util(kUHint);
     const double4 sh = lgeo[hint];
     double ch;
-#if PSRT_ABLATE == 4
-    {
-      double x0 = ox, bt2 = bt, ch2;
-      int bi2 = bi;
-      asm volatile("" : "+v"(x0));
-      test_sphere(sh, hint, x0, oy, oz, dx, dy, dz, A, bt2, bi2, &ch2);
-      PSRT_SINK(bt2); PSRT_SINK(bi2); PSRT_SINK(ch2);
-    }
-#endif
     test_sphere(sh, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, &ch);
     fix = bv.fixpoint && ch == 0.0 && sh.w >= 0x1p-700 && sh.w <= 0x1p700 && am <= 0x1p40;
     ++cs.spheres;
@@ -640,19 +537,6 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
       nbw = lnb[hint];
   }
   clk.mark(kSecQHint);
-#if PSRT_ABLATE == 5
-  {
-    double x0 = ox, bt2 = bt;
-    int bi2 = bi;
-    bool f2 = false;
-    asm volatile("" : "+v"(x0));
-    for (int b = 0; b < bv.n_big; ++b) {
-      const int idx = bv.big_idx[b];
-      if (idx != hint) f2 |= test_sphere(geo[idx], idx, x0, oy, oz, dx, dy, dz, A, bt2, bi2);
-    }
-    PSRT_SINK(bt2); PSRT_SINK(bi2); PSRT_SINK((int)f2);
-  }
-#endif
   for (int b = 0; b < bv.n_big; ++b) {
     const int idx = bv.big_idx[b];
     if (idx != hint) full |= test_sphere(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
@@ -684,15 +568,6 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     // sphere's padded box): coordinates up to ~630 S; admitted up to 256 S
     // (|o| <= 4 r_check, bt |d| <= 4 r_check), else the walk / root-box test
     const double rg = 4.0 * gc.r_check;
-#if PSRT_ABLATE == 6
-    {
-      double x0 = ox;
-      asm volatile("" : "+v"(x0));
-      const int c2 = (am <= rg && (bt * bt) * A <= rg * rg)
-                         ? grid_locate(gc, x0, oy, oz, dx, dy, dz, bt) : kGridNone;
-      PSRT_SINK(c2);
-    }
-#endif
     const int cell = (am <= rg && (bt * bt) * A <= rg * rg)
                          ? grid_locate(gc, ox, oy, oz, dx, dy, dz, bt) : kGridNone;
     listed = cell != kGridNone;
@@ -706,28 +581,6 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
       cnt = bv.cell_start[cell + 1] - e0;
     }
   }
-#if PSRT_ABLATE == 7
-  {
-    double x0 = ox, bt2 = bt;
-    int bi2 = bi;
-    bool f2 = false;
-    uint64_t lo2 = lo, hi2 = hi;
-    asm volatile("" : "+v"(x0));
-    for (int e = 0; e < cnt; ++e) {
-      int idx;
-      if (cam) {
-        lo2 = (lo2 >> 16) | (hi2 << 48);
-        hi2 >>= 16;
-        idx = (int)(lo2 & 0xFFFFu);
-      } else {
-        idx = items[e];
-      }
-      if (idx == hint) continue;
-      f2 |= test_sphere(lgeo[idx], idx, x0, oy, oz, dx, dy, dz, A, bt2, bi2);
-    }
-    PSRT_SINK(bt2); PSRT_SINK(bi2); PSRT_SINK((int)f2);
-  }
-#endif
   for (int e = 0; e < cnt; ++e) {
     clk.util(kUListTrip);
     int idx;
@@ -850,21 +703,7 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
         leaf = leaf_b;
         next = __float_as_int(b1.z);
       } else {
-#if PSRT_TRIP3
-        // node+1 is an interior hit too: its first child node+2 in this trip
-        const float4 c0 = nodes[2 * node + 4], c1 = nodes[2 * node + 5];
-        const int leaf_c = __float_as_int(c1.w);
-        if (!slab_hit(c0, c1, ix, iy, iz, oix, oiy, oiz, tlo, tmax)) {
-          next = __float_as_int(c1.z);
-        } else if (leaf_c >= 0) {
-          leaf = leaf_c;
-          next = __float_as_int(c1.z);
-        } else {
-          next = node + 3;
-        }
-#else
         next = node + 2;
-#endif
       }
       cs.boxes += 2;
       node = next;
@@ -909,35 +748,6 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
   return bi;
 }
 
-#ifndef PSRT_LDS_LEAVES
-#define PSRT_LDS_LEAVES 1  // leaf index + sphere reads from LDS in the walk
-#endif
-
-#ifndef PSRT_RAW_TRIALS
-#define PSRT_RAW_TRIALS 1  // queue raw PCG outputs; the in-sphere test on unscaled doubles
-#endif
-
-#ifndef PSRT_INT_SPHERE
-#define PSRT_INT_SPHERE 0  // random_in_unit_sphere's test in int64 (psrt_device.h); measured slower
-#endif
-
-#ifndef PSRT_TRIP3
-#define PSRT_TRIP3 0  // BVH trips descend up to three levels
-#endif
-
-#ifndef PSRT_QDEPTH
-#define PSRT_QDEPTH 2  // look-ahead queue depth (accepted random_in_unit_sphere trials)
-#endif
-#ifndef PSRT_QFLAGS
-#define PSRT_QFLAGS 1  // depth-2 queue occupancy as two lane masks (no integer count)
-#endif
-static_assert(!PSRT_QFLAGS || PSRT_QDEPTH == 2, "queue flags: depth 2 only");
-static_assert(PSRT_QDEPTH == 2 || PSRT_QDEPTH == 3, "queue slots q0..q2 exist");
-
-#ifndef PSRT_TRACE_WAVES
-#define PSRT_TRACE_WAVES 6  // min waves per SIMD requested from the register allocator
-                            // (6: 80 VGPRs, +2% over 5 despite 4 spilled VGPRs; 7 loses)
-#endif
 
 // rays / sphere tests / box tests of this wave (32-bit per lane) -> one 64-bit
 // atomic each. Called converged (whole wave).
@@ -956,20 +766,8 @@ __device__ __forceinline__ void flush_counters(unsigned long long* ctr, unsigned
   }
 }
 
-// PSRT_BLOCK_DONE measurement builds: add n finished records to 64-pixel block
-// b's counter; the adder that completes the block (ub records) zeroes it.
-__device__ __forceinline__ void block_done_add(const TraceArgs& a, unsigned b, unsigned n) {
-  const unsigned ub = min(64u, a.pixels - 64u * b) * (unsigned)a.s_count;
-  if (PSRT_BLOCK_DONE & 8) {  // no return value: the atomic's issue cost alone
-    __hip_atomic_fetch_add(a.block_done + b, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else if (__hip_atomic_fetch_add(a.block_done + b, n, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT) + n == ub) {
-    __hip_atomic_store(a.block_done + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 template <bool kBVH, bool kStamps, bool kLds, bool kCount>
-__global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(const double4* __restrict__ geo,
+__global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const double4* __restrict__ geo,
                                                           const double* __restrict__ inv_r,
                                                           double* __restrict__ samples,
                                                           TraceArgs a, BvhView bv) {
@@ -1023,16 +821,14 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   const float4* __restrict__ nodes = kLds ? s_nodes : bv.nodes;
   const double4* __restrict__ lgeo = kLds ? s_geo : geo;
   const double* __restrict__ linv = kLds ? s_inv : inv_r;
-  const int* __restrict__ lleaf = (kLds && PSRT_LDS_LEAVES) ? s_leaf : bv.leaf_idx;
+  const int* __restrict__ lleaf = kLds ? s_leaf : bv.leaf_idx;
   const int* __restrict__ lnb = kLds ? s_nb : bv.nb_word;
 
-  // PSRT_BLOCK_DONE & 16: this wave's pending record counts of two blocks
-  [[maybe_unused]] unsigned agg_b0 = ~0u, agg_n0 = 0, agg_b1 = ~0u, agg_n1 = 0;
   // wave-uniform work window
   uint64_t win_base = 0;
   unsigned win_left = 0;
   bool exhausted = false;
-  bool tailp = false;  // exhausted, and the launch's tail runs at PSRT_TAIL_PRIO (a.tail_prio)
+  bool tailp = false;  // exhausted, and the launch's tail runs at kTailPrio (a.tail_prio)
 
   bool active = false;
   bool done = false;  // sample finished; its colour is stored by the next refill block
@@ -1051,16 +847,11 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
   // look-ahead of random_in_unit_sphere (vec3.h:83-95): accepted trials, in
   // stream order, as raw rand() triples (z, y, x draw order)
   uint32_t q0x = 0, q0y = 0, q0z = 0, q1x = 0, q1y = 0, q1z = 0;
-#if PSRT_QDEPTH > 2
-  uint32_t q2x = 0, q2y = 0, q2z = 0;
-#endif
-  int qn = 0;
-  bool qv0 = false, qv1 = false;  // PSRT_QFLAGS: slot 0 / slot 1 hold a trial
+  bool qv0 = false, qv1 = false;  // slot 0 / slot 1 of the queue hold a trial
   double pbt = 0.0;      // closest t / index so far of this ray's world.hit
   int pbi = -1;
   CullStatsT<kCount> cs{0u, 0u};
   unsigned long long traced = 0;  // wave-uniform: rays this wave traced
-  unsigned ablate_sink = 0;       // PSRT_ABLATE measurement builds only
   SectionClock<kStamps> clk;
   __shared__ unsigned s_util[kStamps ? 2 * kUCount : 1];
   if constexpr (kStamps) {
@@ -1114,59 +905,10 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
           kk = (unsigned short)(k < kSampleKCap ? k : kSampleKCap);
         }
         const unsigned u = su;  // < total < 2^32
-#if PSRT_BLOCK_DONE & 1
-        // agent-scope stores (global_store ... sc1): visible to a reducer on
-        // another XCD after its acquire (scripts/sc1_probe.hip)
-        __hip_atomic_store(samples + u, tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((unsigned short*)(samples + total) + u, kk, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-#elif PSRT_NT_STORE
         __builtin_nontemporal_store(tt, samples + u);
         __builtin_nontemporal_store(kk, (unsigned short*)(samples + total) + u);
-#else
-        samples[u] = tt;
-        ((unsigned short*)(samples + total))[u] = kk;  // k array follows the t array
-#endif
         done = false;
       }
-#if PSRT_BLOCK_DONE & 4
-      // Per-block completion accounting of the in-launch reduce (DESIGN.md
-      // §13), measured alone: the records above complete, then one agent-scope
-      // atomic per distinct 64-pixel block among the lanes that stored; the
-      // lane that completes a block zeroes its counter (no reduce yet).
-      {
-        uint64_t m = __ballot(stored);
-        if (m != 0) {
-          if (PSRT_BLOCK_DONE & 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          const unsigned blk = q >> 6;  // 64-pixel block of this lane's record
-          while (m != 0) {
-            const int l0 = __builtin_ctzll(m);
-            const unsigned b0 = __shfl(blk, l0);
-            const uint64_t mine = __ballot(stored && blk == b0);
-            const unsigned n = (unsigned)__popcll(mine);
-            if (PSRT_BLOCK_DONE & 16) {
-              // per-wave aggregation over the (at most two) blocks the wave's
-              // windows currently cover: one atomic when a block leaves the pair
-              if (b0 == agg_b0) {
-                agg_n0 += n;
-              } else if (b0 == agg_b1) {
-                agg_n1 += n;
-              } else {
-                if (lane == 0 && agg_n0) block_done_add(a, agg_b0, agg_n0);
-                agg_b0 = agg_b1, agg_n0 = agg_n1;
-                agg_b1 = b0, agg_n1 = n;
-              }
-            } else if (lane == (unsigned)l0) {
-              block_done_add(a, b0, n);
-            }
-            m &= ~mine;
-          }
-        }
-      }
-#endif
-    }
-    if constexpr (PSRT_REFILL_PRIO > 0) {
-      if (run_block && !exhausted) __builtin_amdgcn_s_setprio(PSRT_REFILL_PRIO);
     }
     if (run_block && !exhausted) {
       const unsigned cnt = (unsigned)__popcll(need_mask);
@@ -1209,24 +951,6 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
           const int j = rc.hm1_i - r;
           const unsigned pix = (unsigned)j * dw.d + i;
           const unsigned s = (unsigned)rc.s_begin + sl;
-#if PSRT_ABLATE == 8
-          {
-            unsigned u2 = (unsigned)unit;
-            asm volatile("" : "+v"(u2));
-            const unsigned q2 = fast_div(u2, ds), r2 = fast_div(q2, dw);
-            const unsigned i2 = q2 - r2 * dw.d;
-            const int j2 = rc.hm1_i - (rc.row_offset + (int)r2 * rc.row_stride);
-            uint64_t g2 = splitmix64((((uint64_t)((unsigned)j2 * dw.d + i2)) << 32 |
-                                      (uint64_t)(rc.s_begin + u2 - q2 * ds.d)) ^ rc.seedmix);
-            const double uu = ((double)i2 + random_double(g2)) / rc.wm1;
-            const double vv = ((double)j2 + random_double(g2)) / rc.hm1;
-            const double* cm = rc.cam;
-            const double ex = ((cm[3] + uu * cm[6]) + vv * cm[9]) - cm[0];
-            const double ey = ((cm[4] + uu * cm[7]) + vv * cm[10]) - cm[1];
-            const double ez = ((cm[5] + uu * cm[8]) + vv * cm[11]) - cm[2];
-            PSRT_SINK((ex * ex + ey * ey) + ez * ez); PSRT_SINK(g2);
-          }
-#endif
           rng = splitmix64((((uint64_t)pix) << 32 | (uint64_t)s) ^ rc.seedmix);
           // main.cc:80-81, camera.h:25-28
           const double u = ((double)i + random_double(rng)) / rc.wm1;
@@ -1239,8 +963,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
           A = (dx * dx + dy * dy) + dz * dz;
           k = 0;
           hint = -1;
-          qn = 0;  // the sample's stream starts here: no look-ahead yet
-          qv0 = qv1 = false;
+          qv0 = qv1 = false;  // the sample's stream starts here: no look-ahead yet
           active = true;
         }
       }
@@ -1255,19 +978,15 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
         exhausted = true;
         // Launch tail: this wave's remaining paths decide when the launch
         // (and the next frame's start on its CUs) ends; let them issue first.
-        if (PSRT_TAIL_PRIO > 0 && a.tail_prio) {
+        if (a.tail_prio) {
           tailp = true;
-          __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
+          __builtin_amdgcn_s_setprio(kTailPrio);
         }
         if constexpr (kStamps) {
           const unsigned long long t = __builtin_amdgcn_s_memrealtime();
           if (wlog && lane == 0) wlog[1] = t, wlog[3] = iters;
         }
       }
-    }
-    if constexpr (PSRT_REFILL_PRIO > 0) {
-      if (PSRT_TAIL_PRIO > 0 && tailp) __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
-      else __builtin_amdgcn_s_setprio(0);
     }
     clk.mark(kSecRefill);
     if (__ballot(active) == 0) break;
@@ -1280,7 +999,7 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
     // SIMD occupancy instead of once per iteration for a handful of lanes.
     bool resolved = false, finish = false;
     traced += (unsigned)__popcll(__ballot(active && !pending && !sc_wait && a.max_depth >= 0));
-    if constexpr (PSRT_HIT_PRIO > 0) __builtin_amdgcn_s_setprio(PSRT_HIT_PRIO);
+    __builtin_amdgcn_s_setprio(kHitPrio);
     if (active && !pending && !sc_wait) {
       if (a.max_depth < 0) {  // main.cc:36-37 at the first call: black, no trace
         finish = true;
@@ -1293,18 +1012,6 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
           unsigned zg = 0;
           asm volatile("" : "+v"(zg));  // re-read the grid constants from LDS here
           const GridC& gc = *(const GridC*)((const char*)&s_gc + zg);
-#if PSRT_ABLATE == 1  // measurement only: the section runs twice, the copy's result sunk
-          {
-            double x0 = ox, x1 = oy, x2 = oz, x3 = dx, x4 = dy, x5 = dz, bt2;
-            asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4), "+v"(x5));
-            int bi2;
-            bool tr2;
-            CullStatsT<kCount> cs2{0u, 0u};
-            const bool r2 = hit_quick(geo, lgeo, a.n, bv, hint, x0, x1, x2, x3, x4, x5, A, bt2,
-                                      bi2, cs2, clk, tr2, q, lnb, gc);
-            ablate_sink += (unsigned)bi2 + (unsigned)r2 + (unsigned)tr2 + (unsigned)(bt2 > 1.0);
-          }
-#endif
           resolved = hit_quick(geo, lgeo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi,
                                cs, clk, trapped, q, lnb, gc);
           pending = !resolved;
@@ -1335,31 +1042,17 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
         }
       }
     }
-    if constexpr (PSRT_HIT_PRIO > 0) {  // back to the base priority
-      if (PSRT_TAIL_PRIO > 0 && tailp) __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
-      else __builtin_amdgcn_s_setprio(0);
-    }
+    if (tailp) __builtin_amdgcn_s_setprio(kTailPrio);  // back to the base priority
+    else __builtin_amdgcn_s_setprio(0);
     clk.mark(kSecHit);
     if constexpr (kBVH) {
       const uint64_t pend = __ballot(pending);
       const uint64_t movable = __ballot(active && !pending);
       if (pend != 0 && ((unsigned)__popcll(pend) >= a.batch || movable == 0)) {
-        if constexpr (PSRT_WALK_PRIO > 0) __builtin_amdgcn_s_setprio(PSRT_WALK_PRIO);
+        __builtin_amdgcn_s_setprio(kWalkPrio);
         if (pending) {
           clk.util(kUWalk);
-#if PSRT_ABLATE == 3  // measurement only: the walk runs twice, the copy's result sunk
-          {
-            double x0 = ox, bt2 = pbt;
-            int bi2 = pbi, n2 = wnode;
-            asm volatile("" : "+v"(x0), "+v"(n2));
-            CullStatsT<kCount> cs2{0u, 0u};
-            hit_traverse<false, kLds && PSRT_LDS_LEAVES>(bv, nodes, lleaf, lgeo, hint, x0, oy,
-                                                         oz, dx, dy, dz, A, bt2, bi2, cs2, n2,
-                                                         movable ? a.walk_tail : 0u);
-            ablate_sink += (unsigned)bi2 + (unsigned)n2 + (unsigned)(bt2 > 1.0);
-          }
-#endif
-          hit_traverse<kStamps, kLds && PSRT_LDS_LEAVES>(bv, nodes, lleaf, lgeo, hint, ox, oy,
+          hit_traverse<kStamps, kLds>(bv, nodes, lleaf, lgeo, hint, ox, oy,
                                                          oz, dx, dy, dz, A, pbt, pbi, cs, wnode,
                                                          movable ? a.walk_tail : 0u);
           if (wnode >= bv.n_nodes) {
@@ -1374,10 +1067,8 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
             }
           }
         }
-        if constexpr (PSRT_WALK_PRIO > 0) {
-          if (PSRT_TAIL_PRIO > 0 && tailp) __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
-          else __builtin_amdgcn_s_setprio(0);
-        }
+        if (tailp) __builtin_amdgcn_s_setprio(kTailPrio);
+        else __builtin_amdgcn_s_setprio(0);
       }
     }
     // depth-0 hit: 0.5 * ray_color(.., -1) = black (main.cc:36-37, 43)
@@ -1402,92 +1093,37 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       // take it (their stream advances), so the draws stay in stream order
       int f = 0;
       do {
-        const bool go = can_fill && (PSRT_QFLAGS ? !qv1 : qn < PSRT_QDEPTH);
+        const bool go = can_fill && !qv1;
         if (go) clk.util(kUTrial);
         uint32_t z, y, x;
         uint64_t nxt;
-#if PSRT_RAW_TRIALS
         raw32_x3(rng, z, y, x, nxt);  // z, y, x: g++'s draw order (vec3.h:78-81); raw outputs
-#else
-        rand31_x3(rng, z, y, x, nxt);  // z, y, x: g++'s draw order (vec3.h:78-81)
-#endif
-#if PSRT_ABLATE == 2  // measurement only: a second trial computed and sunk
-        {
-          uint64_t r2 = rng ^ 0x9E3779B97F4A7C15ULL;
-          asm volatile("" : "+v"(r2));
-          uint32_t z2, y2, x2;
-          uint64_t n2;
-          rand31_x3(r2, z2, y2, x2, n2);
-          const double a2 = pm1_of(z2), b2 = pm1_of(y2), c2 = pm1_of(x2);
-          ablate_sink += (unsigned)!((c2 * c2 + b2 * b2) + a2 * a2 > 1.0) + (unsigned)n2;
-        }
-#endif
-#if PSRT_RAW_TRIALS
         const bool in = in_unit_sphere_raw(x, y, z);
-#elif PSRT_INT_SPHERE
-        const bool in = in_unit_sphere(x, y, z);
-#else
-        const double rz = pm1_of(z), ry = pm1_of(y), rx = pm1_of(x);
-        const bool in = !((rx * rx + ry * ry) + rz * rz > 1.0);
-#endif
         rng = go ? nxt : rng;
         const bool push = go && in;
-        const bool to0 = push && (PSRT_QFLAGS ? !qv0 : qn == 0),
-                   to1 = push && (PSRT_QFLAGS ? qv0 : qn == 1);
+        const bool to0 = push && !qv0, to1 = push && qv0;
         q0x = to0 ? x : q0x, q0y = to0 ? y : q0y, q0z = to0 ? z : q0z;
         q1x = to1 ? x : q1x, q1y = to1 ? y : q1y, q1z = to1 ? z : q1z;
-#if PSRT_QDEPTH > 2
-        const bool to2 = push && qn == 2;
-        q2x = to2 ? x : q2x, q2y = to2 ? y : q2y, q2z = to2 ? z : q2z;
-#endif
-        if (PSRT_QFLAGS) {
-          qv1 = qv1 || to1;
-          qv0 = qv0 || to0;
-        } else {
-          qn += push ? 1 : 0;
-        }
+        qv1 = qv1 || to1;
+        qv0 = qv0 || to0;
         ++f;
       } while (f < a.rng_fill ||
                (f < a.rng_fill + a.rng_extra &&
-                __ballot(want && (PSRT_QFLAGS ? !qv0 : qn == 0)) != 0));
+                __ballot(want && !qv0) != 0));
     }
     clk.mark(kSecFillShade);
 
     // ---- scatter: target = (p + n) + random_in_hemisphere(n)  (main.cc:42-43) ----
-    const bool have = PSRT_QFLAGS ? qv0 : qn > 0;
+    const bool have = qv0;
     sc_wait = want && !have;
-    if constexpr (PSRT_SCATTER_PRIO > 0) __builtin_amdgcn_s_setprio(PSRT_SCATTER_PRIO);
     if (want && have) {
       clk.util(kUScatter);
-#if PSRT_ABLATE == 9
-      {
-        double x0 = ox;
-        asm volatile("" : "+v"(x0));
-        const HitRec h2 = hit_record_of(lgeo[hit], linv[hit], t, x0, oy, oz, dx, dy, dz);
-        double sx = pm1_raw(q0x), sy = pm1_raw(q0y), sz = pm1_raw(q0z);
-        if (!((sx * h2.nx + sy * h2.ny) + sz * h2.nz > 0.0)) sx = -sx, sy = -sy, sz = -sz;
-        const double ex = ((h2.px + h2.nx) + sx) - h2.px, ey = ((h2.py + h2.ny) + sy) - h2.py,
-                     ez = ((h2.pz + h2.nz) + sz) - h2.pz;
-        PSRT_SINK((ex * ex + ey * ey) + ez * ez);
-      }
-#endif
       const HitRec h = hit_record_of(lgeo[hit], linv[hit], t, ox, oy, oz, dx, dy, dz);
       // vec3.h:78-81 random(-1, 1) from the queued draws; vec3.h:102-109 flip
-#if PSRT_RAW_TRIALS
       double rx = pm1_raw(q0x), ry = pm1_raw(q0y), rz = pm1_raw(q0z);
-#else
-      double rx = pm1_of(q0x), ry = pm1_of(q0y), rz = pm1_of(q0z);
-#endif
       q0x = q1x, q0y = q1y, q0z = q1z;
-#if PSRT_QDEPTH > 2
-      q1x = q2x, q1y = q2y, q1z = q2z;
-#endif
-      if (PSRT_QFLAGS) {
-        qv0 = qv1;
-        qv1 = false;
-      } else {
-        --qn;
-      }
+      qv0 = qv1;
+      qv1 = false;
       if (!((rx * h.nx + ry * h.ny) + rz * h.nz > 0.0)) rx = -rx, ry = -ry, rz = -rz;
       dx = ((h.px + h.nx) + rx) - h.px;
       dy = ((h.py + h.ny) + ry) - h.py;
@@ -1496,10 +1132,6 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       A = (dx * dx + dy * dy) + dz * dz;
       hint = hit;
       ++k;
-    }
-    if constexpr (PSRT_SCATTER_PRIO > 0) {
-      if (PSRT_TAIL_PRIO > 0 && tailp) __builtin_amdgcn_s_setprio(PSRT_TAIL_PRIO);
-      else __builtin_amdgcn_s_setprio(0);
     }
     clk.mark(kSecScatter);
 
@@ -1527,11 +1159,6 @@ __global__ __launch_bounds__(kTraceBlock, PSRT_TRACE_WAVES) void psrt_trace(cons
       atomicAdd(a.stamps + 12 + e, (unsigned long long)s_util[e]);
   }
 
-  if (PSRT_ABLATE && ablate_sink == 0x9E3779B9u && a.width < 0) samples[0] = ablate_sink;
-#if PSRT_BLOCK_DONE & 16
-  if (lane == 0 && agg_n0) block_done_add(a, agg_b0, agg_n0);
-  if (lane == 0 && agg_n1) block_done_add(a, agg_b1, agg_n1);
-#endif
   unsigned long long* const ctr = a.ray_counter + kShardStride * (blockIdx.x % kQueues);
   flush_counters(ctr, rays, cs.spheres, cs.boxes, lane);
   if (lane == 0 && traced) {
@@ -1558,15 +1185,8 @@ PSRT_INSTANTIATE(true, true, true)
 
 // pixel_color += sample, in sample order (main.cc:77-84); write_color on the
 // last chunk (color.h:8-24).
-#ifndef PSRT_REDUCE_PREFETCH
-#define PSRT_REDUCE_PREFETCH 1  // psrt_reduce: next tile's loads in flight while summing
-#endif
-#ifndef PSRT_REDUCE_PRIO
-#define PSRT_REDUCE_PRIO 0  // s_setprio of psrt_reduce's waves (they share CUs with the next frame's trace)
-#endif
 
 __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
-  if constexpr (PSRT_REDUCE_PRIO > 0) __builtin_amdgcn_s_setprio(PSRT_REDUCE_PRIO);
   // the trace launch's sharded counter sets -> totals (-> host), then the
   // sets and queue heads back to zero (ReduceArgs; stream order puts this
   // after every trace block and before the context's next launch)
@@ -1601,7 +1221,7 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
   // k per pixel. With s_count % 4 == 0 they are 16-B aligned: t is read in
   // 16-B pieces (kLT lanes per pixel), k in 8-B pieces (kLK lanes per pixel),
   // and the next tile's loads are in flight while this tile is summed from
-  // LDS (PSRT_REDUCE_PREFETCH); else element by element.
+  // LDS; else element by element.
   constexpr int kLT = kReduceTile / 2, kPT = 64 / kLT;  // t: lanes, pixels per load
   constexpr int kLK = kReduceTile / 4, kPK = 64 / kLK;  // k: lanes, pixels per load
   static_assert(kReduceBlock == 64 && (kReduceTile == 16 || kReduceTile == 32),
@@ -1645,9 +1265,8 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
       for (int i = 0; i < kLK; ++i)
         *(uint2*)&s_k[kPK * i + lane / kLK][(lane % kLK) * 4] = vk[i];
       __syncthreads();
-      if (PSRT_REDUCE_PREFETCH && s0 + kReduceTile < S) load(s0 + kReduceTile);
+      if (s0 + kReduceTile < S) load(s0 + kReduceTile);  // next tile in flight
       sum_tile(min((unsigned)kReduceTile, S - s0));
-      if (!PSRT_REDUCE_PREFETCH && s0 + kReduceTile < S) load(s0 + kReduceTile);
     }
   } else {
     for (unsigned s0 = 0; s0 < S; s0 += kReduceTile) {

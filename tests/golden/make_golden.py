@@ -44,15 +44,27 @@ def ref_render(args, rows_total, width, procs=1):
             extra = ["--rows", f"{k}:{procs}"] if procs > 1 else []
             _, st = O.run_ref([*args, *extra, "--accum", acc, "--ppm", os.path.join(td, f"p{k}.ppm")])
             rows = len(range(k, rows_total, procs))
-            return np.fromfile(acc, dtype=np.float64).reshape(rows, width, 3), st["rays"]
+            # the reference's own write_color text (color.h:21-23), one line per pixel
+            body = open(os.path.join(td, f"p{k}.ppm")).read().split("\n", 3)[3]
+            lines = body.splitlines()
+            assert len(lines) == rows * width
+            return (np.fromfile(acc, dtype=np.float64).reshape(rows, width, 3), st["rays"],
+                    [lines[r * width:(r + 1) * width] for r in range(rows)])
         with ThreadPoolExecutor(procs) as ex:
             parts = list(ex.map(one, range(procs)))
     accum = np.zeros((rows_total, width, 3), dtype=np.float64)
-    for k, (a, _) in enumerate(parts):
+    text_rows = [None] * rows_total
+    for k, (a, _, tr) in enumerate(parts):
         accum[k::procs] = a
-    rays = sum(r for _, r in parts)
+        text_rows[k::procs] = tr
+    rays = sum(r for _, r, _ in parts)
+    # The PPM is the reference's own text (main.cc:70 header + write_color
+    # lines of the shards, re-interleaved); the oracle's quantizer must
+    # reproduce it byte for byte (that pins oracle.quantize / ppm_p3 directly).
+    ppm = (f"P3\n{width} {rows_total}\n255\n" + "".join(
+        "".join(l + "\n" for l in row) for row in text_rows)).encode()
     spp = int(args[args.index("--spp") + 1])
-    ppm = O.ppm_p3(O.quantize(accum, spp))
+    assert ppm == O.ppm_p3(O.quantize(accum, spp)), "oracle quantizer differs from write_color"
     return accum, ppm, rays
 
 
