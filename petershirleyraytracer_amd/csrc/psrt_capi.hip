@@ -76,6 +76,10 @@ constexpr size_t kHeads = 128;
 constexpr size_t kSets = kHeads + (size_t)psrt::kQueues * psrt::kShardStride;
 constexpr size_t kCounterWords = kSets + (size_t)psrt::kQueues * psrt::kShardStride;
 
+// HBM left to the GPU's other users when the sample buffer is sized to the
+// free memory (rt_render_device)
+constexpr size_t kHbmReserve = (size_t)256 << 20;
+
 size_t sample_buffer_cap_bytes() {
   const char* e = std::getenv("PSRT_SAMPLE_BUF_MB");
   // default 48 GiB of the 288 GB HBM: C4 on one GPU (41 GB of sample
@@ -557,25 +561,53 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   // sample chunking: the samples buffer holds s_chunk x P records of
   // kSampleBytes (t array, then k array), units < 2^32
   // (chunks of a multiple of 4 samples where possible: psrt_reduce then reads
-  // 16-B aligned runs)
-  size_t s_chunk = sample_buffer_cap_bytes() / (P * psrt::kSampleBytes);
-  if (s_chunk > 4) s_chunk &= ~(size_t)3;
-  if (s_chunk < 1) s_chunk = 1;
-  if (s_chunk > (size_t)p->spp) s_chunk = p->spp;
+  // 16-B aligned runs). The chunk count never changes a bit of the frame:
+  // psrt_reduce continues each pixel's running sum across chunks, in sample
+  // order (main.cc:77-84).
   const size_t s_units = ((1ULL << 32) - 1) / P;  // units of one launch < 2^32
   if (s_units < 1) return set_error(RT_E_INVALID, "shard too large");
-  if (s_chunk > s_units) s_chunk = s_units > 4 ? s_units & ~(size_t)3 : s_units;
-  // the same number of chunks, balanced (no short last chunk with its own tail)
-  const int nchunks = (int)((p->spp + s_chunk - 1) / s_chunk);
-  if (nchunks > 1) {
-    size_t even = ((size_t)p->spp + nchunks - 1) / nchunks;
-    if (even > 4) even = (even + 3) & ~(size_t)3;
-    if (even <= s_chunk) s_chunk = even;
+  // The buffer is sized to the HBM actually free: hipMemGetInfo's free bytes
+  // plus this context's current buffer (it is replaced), less a reserve for
+  // the GPU's other users, capped by PSRT_SAMPLE_BUF_MB.
+  size_t cap_bytes = sample_buffer_cap_bytes();
+  {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+      const size_t usable = fr + c->samples_cap * sizeof(double);
+      cap_bytes = std::min(cap_bytes, usable > kHbmReserve ? usable - kHbmReserve : 0);
+    }
   }
-  // t array (doubles) then k array (uint16), P x s_chunk records each
-  const size_t recs = P * s_chunk;
-  rc = ensure_buf(c, &c->d_samples, &c->samples_cap, recs + (recs + 3) / 4);
-  if (rc) return rc;
+  auto plan = [&](size_t s_max) {
+    size_t sc = s_max;
+    if (sc > 4) sc &= ~(size_t)3;
+    if (sc < 1) sc = 1;
+    if (sc > (size_t)p->spp) sc = p->spp;
+    if (sc > s_units) sc = s_units > 4 ? s_units & ~(size_t)3 : s_units;
+    // the same number of chunks, balanced (no short last chunk with its own tail)
+    const size_t n = ((size_t)p->spp + sc - 1) / sc;
+    if (n > 1) {
+      size_t even = ((size_t)p->spp + n - 1) / n;
+      if (even > 4) even = (even + 3) & ~(size_t)3;
+      if (even <= sc) sc = even;
+    }
+    return sc;
+  };
+  size_t s_chunk = plan(cap_bytes / (P * psrt::kSampleBytes));
+  // t array (doubles) then k array (uint16), P x s_chunk records each. If the
+  // allocation still fails (another process took the memory meanwhile), halve
+  // the chunk and try again.
+  for (;;) {
+    const size_t recs = P * s_chunk;
+    rc = ensure_buf(c, &c->d_samples, &c->samples_cap, recs + (recs + 3) / 4);
+    if (rc == RT_E_NOMEM && s_chunk > 1) {
+      (void)hipGetLastError();  // clear the failed hipMalloc
+      s_chunk = plan(s_chunk / 2);
+      continue;
+    }
+    if (rc) return rc;
+    break;
+  }
+  const int nchunks = (int)((p->spp + s_chunk - 1) / s_chunk);
   double* acc = d_accum;
   if (!acc && nchunks > 1) {
     rc = ensure_buf(c, &c->d_accum_tmp, &c->accum_tmp_cap, P * 3);
