@@ -424,9 +424,12 @@ def main():
         if run["gate"] and step >= 2 and run["dn"] >= 3:
             st.wait_event(done[(step - 2) % run["dn"]])
         if world == 1:
-            ctx.render_device(run["prm"], acc[sl].data_ptr(), rgb_rows[sl].data_ptr(), st.cuda_stream)
-            with torch.cuda.stream(st):  # the frame to the host (main.cc:70,86 emit the image)
-                host_rgb[sl].copy_(rgb_rows[sl], non_blocking=True)
+            # write_color's bytes go straight into pinned host memory
+            # (main.cc:70,86 emit the image): psrt_reduce stores them across
+            # the link, so the frame's device-to-host transfer is inside the
+            # render and needs no copy of its own (which, as a kernel, would
+            # wait for a CU slot behind the next frame's persistent launch)
+            ctx.render_device(run["prm"], acc[sl].data_ptr(), host_rgb[sl].data_ptr(), st.cuda_stream)
             done[sl].record(st)
             frame = acc[sl]
             pending[sl] = (step, None)
@@ -532,7 +535,7 @@ def main():
     elapsed = timed(depth, args.warmup, args.steps, tail_prio, gated)
     last_slot = (args.warmup + args.steps - 1) % depth
     if world == 1:
-        rgb = rgb_rows[last_slot]
+        rgb = host_rgb[last_slot]
     # Kernel time for the roofline: frames one at a time (in flight together,
     # a launch's HIP events also span the other frame's work).
     unpiped = None
@@ -659,7 +662,8 @@ def main():
             "unpipelined": unpiped,
             "per_rank": per_rank,
             "timed_step": ("render + write_color + " + ("RCCL uint8 gather + " if world > 1 and not args.gather_fp64 else "RCCL FP64 gather + psrt_quantize + " if world > 1 else "")
-                           + "D2H of the frame's bytes into pinned host memory (rank 0)"),
+                           + ("D2H of the frame's bytes into pinned host memory (rank 0)" if world > 1 else
+                              "D2H: psrt_reduce writes the frame's bytes into pinned host memory")),
             # one-time costs, outside the timed steps
             "one_time_ms": {"set_scene": round(scene_ms[0], 3),
                             "camera_lists": round(camlist_ms, 3),
@@ -684,6 +688,16 @@ def main():
         out["parity_vs_cpu"] = parity
         print(json.dumps(out), flush=True)
 
+    # Teardown order matters: torch's pinned-host allocator keeps an event on
+    # each stream a copy into host_rgb ran on (the contexts' own streams), so
+    # those buffers go before close() destroys the streams.
+    torch.cuda.synchronize(dev)
+    host_rgb = None
+    done.clear()
+    streams.clear()
+    import gc
+    gc.collect()
+    torch.cuda.synchronize(dev)
     for c in ctxs:
         c.close()
     if distributed:

@@ -1294,21 +1294,32 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
       sum_tile(T);
     }
   }
-  if (q >= a.pixels) return;
-  if (a.accum) {
+  if (a.accum && q < a.pixels) {
     a.accum[(size_t)q * 3 + 0] = r;
     a.accum[(size_t)q * 3 + 1] = g;
     a.accum[(size_t)q * 3 + 2] = b;
   }
-  if (a.rgb8) {
+  if (a.rgb8) {  // write_color (color.h:8-24)
+    __shared__ __attribute__((aligned(16))) unsigned char s_rgb[kReduceBlock * 3];
     const double inv = 1.0 / (double)a.spp_total;
-    double c[3] = {r, g, b};
+    const double c[3] = {r, g, b};
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
       double x = __builtin_sqrt(c[ch] * inv);
       x = (x < 0.0) ? 0.0 : x;  // std::max(x, 0.0)
       x = (0.999 < x) ? 0.999 : x;  // std::min(x, 0.999)
-      a.rgb8[(size_t)q * 3 + ch] = (unsigned char)(int)(255.999 * x);
+      s_rgb[lane * 3 + ch] = (unsigned char)(int)(255.999 * x);
+    }
+    __syncthreads();
+    // The wave's pixels are 192 contiguous bytes: written as 12 x 16-B stores
+    // (the frame may be pinned host memory, written across the link: the
+    // frame's device-to-host transfer then needs no copy of its own)
+    unsigned char* const dst = a.rgb8 + (size_t)q0 * 3;
+    const unsigned nb = min((unsigned)kReduceBlock, a.pixels - q0) * 3u;
+    if (nb == kReduceBlock * 3u && ((uintptr_t)dst & 15u) == 0) {
+      if (lane < kReduceBlock * 3 / 16) ((uint4*)dst)[lane] = ((const uint4*)s_rgb)[lane];
+    } else {
+      for (unsigned e = lane; e < nb; e += kReduceBlock) dst[e] = s_rgb[e];
     }
   }
 }

@@ -135,3 +135,30 @@ def test_empty_shard(oracle_mod):
     want, _, _ = oracle_mod.render(two, cam, 16, 3, 2)
     assert np.array_equal(bits(out.cpu().numpy()), bits(want))
     ctx.close()
+
+
+def test_render_into_pinned_host_memory():
+    """write_color's bytes may go straight to pinned host memory (bench.py's
+    timed step: psrt_reduce's 16-B stores across the link are the frame's
+    device-to-host transfer): same bytes as a device buffer, for a frame whose
+    row width makes the last wave partial and the 16-B path both taken."""
+    import torch
+    sph = P.scene_random_spheres(1)
+    for (w, h) in ((96, 64), (37, 11)):
+        cam = P.camera_look_at(aspect=w / h)
+        ctx = P.Context(0)
+        ctx.set_scene(sph, cam)
+        dev = torch.zeros((h, w, 3), dtype=torch.uint8, device="cuda:0")
+        host = torch.zeros((h, w, 3), dtype=torch.uint8, pin_memory=True)
+        acc = torch.zeros((h, w, 3), dtype=torch.float64, device="cuda:0")
+        prm = P.params(w, h, 4)
+        ctx.render_device(prm, acc.data_ptr(), dev.data_ptr(), 0)
+        ctx.sync_stats()
+        ctx.render_device(prm, acc.data_ptr(), host.data_ptr(), 0)
+        ctx.sync_stats()
+        torch.cuda.synchronize()
+        assert np.array_equal(dev.cpu().numpy(), host.numpy()), (w, h)
+        want, rgb, _ = P.render(sph, cam, w, h, 4)
+        assert np.array_equal(host.numpy(), rgb), (w, h)
+        del host
+        ctx.close()
