@@ -104,11 +104,12 @@ def parse():
                          "(default: each rank quantises its rows, uint8 gather)")
     ap.add_argument("--no-fixpoint", action="store_true",
                     help="trace provably trapped paths to max_depth (DESIGN.md §9)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="frames per trace launch (rt_render_device_frames, <= 32; 0 = auto: "
+                         "all timed frames in as few launches as fit, 1 for multi-chunk frames)")
     ap.add_argument("--pipeline", type=int, default=0,
-                    help="frames in flight (1 = each frame waits for the previous one; "
-                         "0 = auto: 1 for multi-chunk frames, else 3)")
-    ap.add_argument("--gate", action="store_true",
-                    help="with --pipeline >= 3: frame k's trace waits on the device for frame k-2")
+                    help="launches in flight (0 = auto: measured among 1..3 for one-frame "
+                         "launches of single-chunk frames, else 1)")
     ap.add_argument("--scaling", default="strong", choices=("weak", "strong"),
                     help="strong (default): the configured frame on any N; weak (study): "
                          "N GPUs render the frame at N x spp (per-GPU work fixed)")
@@ -367,23 +368,35 @@ def main():
     # the counting kernel variant (sphere / box tests executed), for one untimed frame
     prm_count = P.params(w, h, spp, args.max_depth, args.seed, off, stride,
                          flags | FLAG_CULL_STATS)
-    # Frames in flight. Two persistent launches that share the GPU for their
-    # whole run are slower than one after the other (C4: -8%), so a frame of
-    # several sample chunks runs alone (depth 1). Otherwise the depth is
-    # picked by measurement on this GPU (`tuning` below, untimed runs).
+    # Frames per launch (--batch; 0 = auto). rt_render_device_frames renders
+    # B frames (seeds seed .. seed + B - 1: the same scene and workload, a new
+    # sample stream each) in one trace launch, so the launch tail (the last
+    # waves' longest paths) is paid once per B frames instead of
+    # once per frame. Auto: every timed frame in as few launches as the 32-bit
+    # unit ids, the sample buffer and kMaxFrames (32) allow; frames of several
+    # sample chunks (C4, C5 on one GPU) go one per launch.
     per_rank = rows * w * spp
     buf_cap = int(os.environ.get("PSRT_SAMPLE_BUF_MB", "49152")) << 20  # psrt_capi.hip
-    # candidates: (frames in flight, tail priority, gated); gated = a frame's
-    # trace waits on the device for frame - 2 to finish (--gate; measured, no
-    # better than ungated: DESIGN.md §7)
-    if args.pipeline > 0:
-        candidates = [(args.pipeline, True, args.gate)]
-    elif per_rank * SAMPLE_RECORD_BYTES > buf_cap or per_rank >= (1 << 30):
-        # several sample chunks, or a frame so long (C4 on one GPU: 560 ms)
-        # that its ~0.5 ms tail is noise: one frame at a time, no tuning runs
-        candidates = [(1, True, False)]
+    multi_chunk = per_rank * SAMPLE_RECORD_BYTES > buf_cap or per_rank >= (1 << 30)
+    if args.batch > 0:
+        B = min(args.batch, 32)
+    elif multi_chunk or per_rank == 0:
+        B = 1
     else:
-        candidates = [(1, True, False), (2, True, False), (3, True, False)]
+        B = max(1, min(32, args.steps, ((1 << 32) - 1) // per_rank,
+                       buf_cap // (per_rank * SAMPLE_RECORD_BYTES)))
+    # Frames in flight (one frame per launch only): each slot has its own
+    # context (work queue, sample buffer, stats), stream and output rows, so
+    # frame k+1 fills the CUs that frame k's last waves release.
+    # Two persistent launches that share the GPU for their whole run are slower
+    # than one after the other, so batches and multi-chunk frames run one at a
+    # time; otherwise the depth is picked by measurement (`tuning` below).
+    if args.pipeline > 0:
+        candidates = [(args.pipeline, True)]
+    elif B > 1 or multi_chunk:
+        candidates = [(1, True)]
+    else:
+        candidates = [(1, True), (2, True), (3, True)]
     depth = max(c[0] for c in candidates)  # contexts / buffers to allocate
     ctxs = []
     scene_ms = []  # rt_context_set_scene: host BVH / grid / neighbour lists + uploads
@@ -394,13 +407,15 @@ def main():
         scene_ms.append((time.perf_counter() - t0) * 1e3)
         ctxs.append(c)
     dev = torch.device("cuda", local)
-    acc = [torch.zeros((rows, w, 3), dtype=torch.float64, device=dev) for _ in range(depth)]
+    # per slot: B frames' accumulators and bytes
+    acc = [torch.zeros((B, rows, w, 3), dtype=torch.float64, device=dev) for _ in range(depth)]
     rgb = torch.zeros((h, w, 3), dtype=torch.uint8, device=dev) if rank == 0 and world > 1 else None
-    rgb_rows = [torch.zeros((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(depth)]
+    rgb_rows = [torch.zeros((B, rows, w, 3), dtype=torch.uint8, device=dev)
+                for _ in range(depth)] if world > 1 else None
     # every step ends with the frame's bytes in pinned host memory (rank 0):
-    # one buffer per frame slot, so frames in flight never share one
+    # per slot and frame, so frames in flight never share one
     host_rows = h if world > 1 else rows
-    host_rgb = [torch.empty((host_rows, w, 3), dtype=torch.uint8, pin_memory=True)
+    host_rgb = [torch.empty((B, host_rows, w, 3), dtype=torch.uint8, pin_memory=True)
                 for _ in range(depth)] if rank == 0 else None
     # each frame slot renders on its context's own stream
     streams = [torch.cuda.ExternalStream(c.stream(), device=dev) for c in ctxs]
@@ -411,85 +426,94 @@ def main():
         if distributed:
             dist.barrier()
 
-    frame = None
-    pending = [None] * depth  # per slot: (step, event after the frame's gather)
-    run = {"dn": depth, "warm": args.warmup, "kms": [], "rays": [], "exec": [], "prm": prm,
-           "gate": False}
-    done = [torch.cuda.Event() for _ in range(depth)]  # per slot: after the frame's render
+    pending = [None] * depth  # per slot: (timed?, event after the gathers, frames)
+    run = {"dn": depth, "kms": [], "rays": [], "exec": [], "frames": [], "prm": prm}
 
-    def launch(step):
-        nonlocal frame
-        sl = step % run["dn"]
+    def ptrs(t, nb):
+        return [t[f].data_ptr() for f in range(nb)]
+
+    def launch(i, nb, is_timed):
+        """Launch i of a timed() sequence: nb frames in one rt_render_device_frames."""
+        sl = i % run["dn"]
         ctx, st = ctxs[sl], streams[sl]
-        if run["gate"] and step >= 2 and run["dn"] >= 3:
-            st.wait_event(done[(step - 2) % run["dn"]])
         if world == 1:
             # write_color's bytes go straight into pinned host memory
             # (main.cc:70,86 emit the image): psrt_reduce stores them across
             # the link, so the frame's device-to-host transfer is inside the
             # render and needs no copy of its own (which, as a kernel, would
             # wait for a CU slot behind the next frame's persistent launch)
-            ctx.render_device(run["prm"], acc[sl].data_ptr(), host_rgb[sl].data_ptr(), st.cuda_stream)
-            done[sl].record(st)
-            frame = acc[sl]
-            pending[sl] = (step, None)
+            ctx.render_device_frames(run["prm"], nb, ptrs(acc[sl], nb), ptrs(host_rgb[sl], nb),
+                                     st.cuda_stream)
+            pending[sl] = (is_timed, None, nb)
             return
         if args.gather_fp64:
-            ctx.render_device(run["prm"], acc[sl].data_ptr(), 0, st.cuda_stream)
-            done[sl].record(st)
+            ctx.render_device_frames(run["prm"], nb, ptrs(acc[sl], nb), None, st.cuda_stream)
             src = acc[sl]
         else:
             # write_color is per pixel: each rank quantises its own rows, and
             # the gather moves 3 B per pixel instead of 24 (C3: 2.9 MB, not 23)
-            ctx.render_device(run["prm"], acc[sl].data_ptr(), rgb_rows[sl].data_ptr(), st.cuda_stream)
-            done[sl].record(st)
+            ctx.render_device_frames(run["prm"], nb, ptrs(acc[sl], nb), ptrs(rgb_rows[sl], nb),
+                                     st.cuda_stream)
             src = rgb_rows[sl]
         comm.wait_stream(st)
         with torch.cuda.stream(comm):
-            frame = gather_frame(src, h, rank, world)
-            if rank == 0:
-                if args.gather_fp64:
-                    ctxs[sl].quantize_device(frame.data_ptr(), w, h, spp, rgb.data_ptr(),
-                                             comm.cuda_stream)
-                else:
-                    rgb.copy_(frame)
-                host_rgb[sl].copy_(rgb, non_blocking=True)
+            for f in range(nb):
+                fr = gather_frame(src[f], h, rank, world)
+                if rank == 0:
+                    if args.gather_fp64:
+                        ctxs[sl].quantize_device(fr.data_ptr(), w, h, spp, rgb.data_ptr(),
+                                                 comm.cuda_stream)
+                    else:
+                        rgb.copy_(fr)
+                    host_rgb[sl][f].copy_(rgb, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(comm)
-        pending[sl] = (step, ev)
+        pending[sl] = (is_timed, ev, nb)
 
     def retire(sl):
-        """Wait for the slot's frame (render + gather) and collect its stats."""
+        """Wait for the slot's launch (render + gathers) and collect its stats."""
         if pending[sl] is None:
             return
-        step, ev = pending[sl]
+        is_timed, ev, nb = pending[sl]
         st = ctxs[sl].sync_stats()
         if ev is not None:
             ev.synchronize()
         pending[sl] = None
-        if step >= run["warm"]:
+        if is_timed:
             run["kms"].append(st["kernel_ms"])
             run["rays"].append(st["rays"])
-            run["exec"].append((st["tests_executed"], st["box_tests"], st["rays_traced"]))
+            run["frames"].append(nb)
+            run["exec"].append((st["tests_executed"], st["box_tests"], st["rays_traced"], nb))
 
     def drain():
         for k in range(depth):
             retire(k)
         torch.cuda.synchronize(dev)
 
-    def timed(dn, nwarm, nsteps, tail=True, gate=False, count=False):
-        """nwarm untimed + nsteps timed frames, dn in flight; the timed frames
-        start from an idle GPU and end when the last one is done."""
-        run.update(dn=dn, warm=nwarm, kms=[], rays=[], exec=[],
-                   prm=prm_count if count else (prm if tail else prm_notail), gate=gate)
-        for step in range(nwarm + nsteps):
-            if step == nwarm:
+    def batches(n, b):
+        out = []
+        while n > 0:
+            out.append(min(b, n))
+            n -= out[-1]
+        return out
+
+    def timed(dn, nwarm, nsteps, b=None, tail=True, count=False):
+        """nwarm untimed + nsteps timed frames in launches of up to b frames,
+        dn launches in flight; the timed frames start from an idle GPU and end
+        when the last one is done."""
+        b = b or B
+        run.update(dn=dn, kms=[], rays=[], exec=[], frames=[],
+                   prm=prm_count if count else (prm if tail else prm_notail))
+        seq = [(nb, False) for nb in batches(nwarm, b)] + [(nb, True) for nb in batches(nsteps, b)]
+        t0 = None
+        for i, (nb, is_timed) in enumerate(seq):
+            if is_timed and t0 is None:
                 drain()
                 barrier()
                 torch.cuda.synchronize(dev)
                 t0 = time.perf_counter()
-            retire(step % dn)  # the slot's previous frame must be done
-            launch(step)
+            retire(i % dn)  # the slot's previous launch must be done
+            launch(i, nb, is_timed)
         drain()
         barrier()
         el = time.perf_counter() - t0
@@ -504,7 +528,7 @@ def main():
     # cached (psrt_capi.hip): that render's non-trace device time minus a
     # cached render's
     def one(ctx, sl):
-        ctx.render_device(prm, acc[sl].data_ptr(), rgb_rows[sl].data_ptr(), streams[sl].cuda_stream)
+        ctx.render_device_frames(prm, 1, [acc[sl][0].data_ptr()], None, streams[sl].cuda_stream)
         return ctx.sync_stats()
     first = one(ctxs[0], 0)
     again = one(ctxs[0], 0)
@@ -514,51 +538,57 @@ def main():
         one(ctxs[k], k)
     torch.cuda.synchronize(dev)
 
-    # untimed tuning runs: every candidate (depth, tail priority) renders
-    # full frames; the fastest (max over ranks) is the one timed below
-    def cname(c):
-        return f"{c[0]}" + ("" if c[1] else "-notail") + ("-gated" if c[2] else "")
+    # untimed tuning runs (one frame per launch only): every candidate depth
+    # renders full frames; the fastest (max over ranks) is the one timed below
     tuning = {}
     if len(candidates) > 1:
         for c in candidates:
             nt = max(6, 2 * c[0])
-            tuning[cname(c)] = timed(c[0], 1, nt, c[1], c[2]) / nt * 1e3
-    # Frames in flight only for a clear gain (> 3% in the tuning runs): with
-    # C3's long frames the tail is worth ~2.5% at best, and a pipelined run
-    # can settle into a schedule where two traces share the GPU and lose more
-    # (DESIGN.md §7); C1 / C2 frames gain 8% to 2x
-    depth, tail_prio, gated = candidates[0]
+            tuning[str(c[0])] = timed(c[0], 1, nt, 1, c[1]) / nt * 1e3
+    # Frames in flight only for a clear gain (> 3% in the tuning runs): a
+    # pipelined run can settle into a schedule where two traces share the GPU
+    # and lose more
+    depth, tail_prio = candidates[0]
     if tuning:
-        best = min(candidates, key=lambda c: tuning[cname(c)])
-        if tuning[cname(best)] < 0.97 * tuning[cname(candidates[0])]:
-            depth, tail_prio, gated = best
-    elapsed = timed(depth, args.warmup, args.steps, tail_prio, gated)
-    last_slot = (args.warmup + args.steps - 1) % depth
-    if world == 1:
-        rgb = host_rgb[last_slot]
-    # Kernel time for the roofline: frames one at a time (in flight together,
-    # a launch's HIP events also span the other frame's work).
+        best = min(candidates, key=lambda c: tuning[str(c[0])])
+        if tuning[str(best[0])] < 0.97 * tuning[str(candidates[0][0])]:
+            depth, tail_prio = best
+    elapsed = timed(depth, args.warmup, args.steps, B, tail_prio)
+    kernel_ms = sum(run["kms"]) / sum(run["frames"])  # device time of the trace per frame
+    rays = sum(run["rays"]) / sum(run["frames"])      # reference rays per frame
+    # The same frames one per launch (the unbatched rate, for comparison), and
+    # the kernel time for the roofline from one-frame launches one at a time
+    # when frames were in flight (their HIP events then span the other frames).
+    unbatched = None
+    if B > 1:
+        n1 = min(args.steps, 5)
+        el1 = timed(1, 1, n1, 1)
+        unbatched = {"ms_per_step": round(el1 / n1 * 1e3, 3),
+                     "value": round((rows if args.emulate_shard else h) * w * spp * n1 / el1 / 1e6, 4),
+                     "kernel_ms": round(sum(run["kms"]) / sum(run["frames"]), 3)}
     unpiped = None
     if depth > 1:
         n1 = min(args.steps, 3)
-        el1 = timed(1, 0, n1)
+        el1 = timed(1, 0, n1, 1)
+        kernel_ms = sum(run["kms"]) / sum(run["frames"])
         unpiped = {"ms_per_step": round(el1 / n1 * 1e3, 3),
                    "value": round((rows if args.emulate_shard else h) * w * spp * n1 / el1 / 1e6, 4)}
-    kernel_ms, rays = run["kms"], run["rays"]
     # Sphere / box tests executed: the timed kernel does not count them (two
     # fewer live registers in its loop), so one untimed frame of the counting
-    # variant (RT_FLAG_CULL_STATS) supplies them; the work is deterministic.
-    timed(1, 0, 1, count=True)
+    # variant (RT_FLAG_CULL_STATS, seed `--seed`: frame 0 of every batch)
+    # supplies them; the work is deterministic.
+    timed(1, 0, 1, 1, count=True)
     executed = run["exec"]
     if world == 1:
-        frame = acc[last_slot]
+        frame = acc[0][0]  # seed --seed (the counting frame above)
+        rgb = host_rgb[0][0]
 
     # an emulated shard processed only its own rows
     total_samples = (rows if args.emulate_shard else h) * w * spp * args.steps
     value = total_samples / elapsed / 1e6
 
     # per-rank kernel time and HBM fraction (rank 0 reports them all)
-    my_kms = float(np.mean(kernel_ms)) if kernel_ms else 0.0
+    my_kms = float(kernel_ms)
     my_hbm = rows * w * spp * SAMPLE_RECORD_BYTES / (my_kms * 1e-3) / PEAK_HBM if my_kms else 0.0
     per_rank = [dict(rank=0, rows=rows, kernel_ms=round(my_kms, 3), hbm_frac=round(my_hbm, 6))]
     if distributed:
@@ -574,20 +604,20 @@ def main():
     # with the reference itself
     gathered = None
     if world > 1:
-        ctxs[0].render_device(prm, acc[0].data_ptr(), 0, streams[0].cuda_stream)
+        ctxs[0].render_device(prm, acc[0][0].data_ptr(), 0, streams[0].cuda_stream)
         ctxs[0].sync_stats()
         torch.cuda.synchronize(dev)
-        gathered = gather_frame(acc[0], h, rank, world)
+        gathered = gather_frame(acc[0][0], h, rank, world)
         torch.cuda.synchronize(dev)
 
     if rank == 0:
         n = len(spheres)
-        avg_ms = float(np.mean(kernel_ms))
-        rays_launch = float(np.mean(rays))  # this rank's rays per launch
+        avg_ms = float(kernel_ms)  # psrt_trace device time per frame (launch / frames in it)
+        rays_launch = float(rays)  # this rank's reference rays per frame
         tests = rays_launch * n  # sphere::hit calls of the reference algorithm
-        ex_tests = float(np.mean([e[0] for e in executed]))
-        ex_boxes = float(np.mean([e[1] for e in executed]))
-        ex_rays = float(np.mean([e[2] for e in executed]))
+        ex_tests = float(np.sum([e[0] for e in executed])) / sum(e[3] for e in executed)
+        ex_boxes = float(np.sum([e[1] for e in executed])) / sum(e[3] for e in executed)
+        ex_rays = float(np.sum([e[2] for e in executed])) / sum(e[3] for e in executed)
         # Algorithmic FP64 work of psrt_trace as executed, in FP64-op slots: 18
         # per exact sphere test (17 FP64 ops + compare: the reference's 23-op
         # test with A hoisted per ray and r*r per sphere, identical values), 7
@@ -628,7 +658,7 @@ def main():
                 "frac": round(achieved / PEAK_FP64_OPS, 4),
                 "traffic": traffic,
                 "kernel": "psrt_trace",
-                "avg_launch_ms": round(avg_ms, 3),
+                "avg_launch_ms": round(avg_ms, 3),  # per frame: launch time / frames per launch
                 "rays_per_launch": int(rays_launch),
                 "rays_traced_per_launch": int(ex_rays),
                 "reference_sphere_tests_per_launch": int(tests),
@@ -653,15 +683,18 @@ def main():
                 # issue is the bound; frac above counts only the FP64 algorithm
                 "valu_issue": valu_issue,
             },
-            "rays_per_sample": round(float(np.sum(rays)) / (rows * w * spp * len(rays)), 3),
+            "rays_per_sample": round(float(rays) / (rows * w * spp), 3),
+            "frames_per_launch": B,
+            # the same frames one per launch (rt_render_device)
+            "unbatched": unbatched,
             "frames_in_flight": depth,
             "tail_priority": tail_prio,
-            "gated": gated,
             "depth_tuning_ms": {k: round(v, 3) for k, v in tuning.items()} or None,
             # the same frames rendered one at a time (each waits for the last)
             "unpipelined": unpiped,
             "per_rank": per_rank,
-            "timed_step": ("render + write_color + " + ("RCCL uint8 gather + " if world > 1 and not args.gather_fp64 else "RCCL FP64 gather + psrt_quantize + " if world > 1 else "")
+            "timed_step": ((f"{B} frames (seeds {args.seed}..{args.seed + B - 1}) per trace launch: " if B > 1 else "")
+                           + "render + write_color + " + ("RCCL uint8 gather + " if world > 1 and not args.gather_fp64 else "RCCL FP64 gather + psrt_quantize + " if world > 1 else "")
                            + ("D2H of the frame's bytes into pinned host memory (rank 0)" if world > 1 else
                               "D2H: psrt_reduce writes the frame's bytes into pinned host memory")),
             # one-time costs, outside the timed steps
@@ -693,7 +726,6 @@ def main():
     # those buffers go before close() destroys the streams.
     torch.cuda.synchronize(dev)
     host_rgb = None
-    done.clear()
     streams.clear()
     import gc
     gc.collect()

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 /* ---- error codes ---------------------------------------------------------- */
 #define RT_OK 0
@@ -154,6 +154,18 @@ int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres,
  * reading. rt_context_sync_stats() reports the finished call's counters. */
 int rt_render_device(rt_context* ctx, const rt_params* params, double* d_accum,
                      unsigned char* d_rgb8, void* stream);
+
+/* Enqueue nframes (1..32) renders of the owned rows in one trace launch per
+ * sample chunk: frame f is the frame of seed params->seed + f (the same
+ * scene, camera and shard; bit-identical to rt_render_device with that
+ * seed) and writes d_accum[f] / d_rgb8[f] (arrays of nframes device pointers,
+ * either array or any entry may be NULL). The launch's tail (the last waves'
+ * paths) is paid once per batch instead of once per frame.
+ * rt_context_sync_stats() reports the batch's totals. rt_render_device is
+ * this call with nframes = 1. */
+int rt_render_device_frames(rt_context* ctx, const rt_params* params, int nframes,
+                            double* const* d_accum, unsigned char* const* d_rgb8,
+                            void* stream);
 
 /* The context's own stream (hipStream_t as void*, non-blocking), used when
  * rt_render_device gets stream == NULL. One context per frame in flight

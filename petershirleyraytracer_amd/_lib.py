@@ -17,7 +17,7 @@ ERRORS = {-1: "RT_E_INVALID", -2: "RT_E_HIP", -3: "RT_E_NODEVICE", -4: "RT_E_NOM
 # Every symbol include/rt.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "rt_rows_owned", "rt_render", "rt_quantize_ppm", "rt_context_create", "rt_context_destroy",
-    "rt_context_set_scene", "rt_render_device", "rt_context_stream", "rt_context_sync_stats", "rt_quantize_device",
+    "rt_context_set_scene", "rt_render_device", "rt_render_device_frames", "rt_context_stream", "rt_context_sync_stats", "rt_quantize_device",
     "rt_camera_default", "rt_camera_look_at", "rt_scene_two_spheres", "rt_scene_random_spheres",
     "rt_scene_parse", "rt_scene_load", "rt_scene_format",
     "rt_last_error", "rt_abi_version", "rt_device_count", "rt_build_info", "rt_debug_probe_f64",
@@ -86,6 +86,8 @@ def load(build_if_missing: bool = False):
         "rt_context_set_scene": ([C.c_void_p, P(RtSphere), C.c_int, P(RtCamera)], C.c_int),
         "rt_render_device": ([C.c_void_p, P(RtParams), C.c_void_p, C.c_void_p, C.c_void_p],
                              C.c_int),
+        "rt_render_device_frames": ([C.c_void_p, P(RtParams), C.c_int, P(C.c_void_p),
+                                     P(C.c_void_p), C.c_void_p], C.c_int),
         "rt_context_sync_stats": ([C.c_void_p, P(RtStats)], C.c_int),
         "rt_context_stream": ([C.c_void_p], C.c_void_p),
         "rt_quantize_device": ([C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,

@@ -532,9 +532,20 @@ static void queue_phases(psrt::TraceArgs& ta, int grid, bool guided) {
 
 int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigned char* d_rgb8,
                      void* stream_) {
+  return rt_render_device_frames(c, p, 1, d_accum ? &d_accum : nullptr,
+                                 d_rgb8 ? &d_rgb8 : nullptr, stream_);
+}
+
+int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
+                            double* const* d_accum_f, unsigned char* const* d_rgb8_f,
+                            void* stream_) {
   if (!c) return set_error(RT_E_INVALID, "rt_render_device: ctx is NULL");
   int rc = check_params(p);
   if (rc) return rc;
+  if (nframes < 1 || nframes > psrt::kMaxFrames)
+    return set_error(RT_E_INVALID, "rt_render_device_frames: nframes %d outside [1, %d]", nframes,
+                     psrt::kMaxFrames);
+  const size_t nf = (size_t)nframes;  // frames of the batch
   if (c->n < 0) return set_error(RT_E_SCENE, "rt_render_device: no scene set");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = stream_ ? (hipStream_t)stream_ : c->stream;
@@ -564,7 +575,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   // 16-B aligned runs). The chunk count never changes a bit of the frame:
   // psrt_reduce continues each pixel's running sum across chunks, in sample
   // order (main.cc:77-84).
-  const size_t s_units = ((1ULL << 32) - 1) / P;  // units of one launch < 2^32
+  const size_t s_units = ((1ULL << 32) - 1) / (P * nf);  // units of one launch < 2^32
   if (s_units < 1) return set_error(RT_E_INVALID, "shard too large");
   // The buffer is sized to the HBM actually free: hipMemGetInfo's free bytes
   // plus this context's current buffer (it is replaced), less a reserve for
@@ -592,12 +603,12 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     }
     return sc;
   };
-  size_t s_chunk = plan(cap_bytes / (P * psrt::kSampleBytes));
+  size_t s_chunk = plan(cap_bytes / (nf * P * psrt::kSampleBytes));
   // t array (doubles) then k array (uint16), P x s_chunk records each. If the
   // allocation still fails (another process took the memory meanwhile), halve
   // the chunk and try again.
   for (;;) {
-    const size_t recs = P * s_chunk;
+    const size_t recs = nf * P * s_chunk;
     rc = ensure_buf(c, &c->d_samples, &c->samples_cap, recs + (recs + 3) / 4);
     if (rc == RT_E_NOMEM && s_chunk > 1) {
       (void)hipGetLastError();  // clear the failed hipMalloc
@@ -608,11 +619,21 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     break;
   }
   const int nchunks = (int)((p->spp + s_chunk - 1) / s_chunk);
-  double* acc = d_accum;
-  if (!acc && nchunks > 1) {
-    rc = ensure_buf(c, &c->d_accum_tmp, &c->accum_tmp_cap, P * 3);
+  // per frame: its accumulators (a scratch block when the caller passes none
+  // and the running sums must survive between sample chunks) and its bytes
+  std::vector<double*> acc(nf, nullptr);
+  std::vector<unsigned char*> rgb(nf, nullptr);
+  bool need_tmp = false;
+  for (size_t f = 0; f < nf; ++f) {
+    acc[f] = d_accum_f ? d_accum_f[f] : nullptr;
+    rgb[f] = d_rgb8_f ? d_rgb8_f[f] : nullptr;
+    need_tmp = need_tmp || (!acc[f] && nchunks > 1);
+  }
+  if (need_tmp) {
+    rc = ensure_buf(c, &c->d_accum_tmp, &c->accum_tmp_cap, nf * P * 3);
     if (rc) return rc;
-    acc = c->d_accum_tmp;
+    for (size_t f = 0; f < nf; ++f)
+      if (!acc[f]) acc[f] = c->d_accum_tmp + f * P * 3;
   }
   rc = ensure_events(c, nchunks);
   if (rc) return rc;
@@ -631,7 +652,9 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   ta.row_offset = p->row_offset;
   ta.row_stride = p->row_stride;
   ta.pixels = (unsigned)P;
-  ta.seedmix = splitmix64_host(p->seed);
+  ta.frames = nframes;
+  for (int f = 0; f < nframes; ++f) ta.seedmix[f] = splitmix64_host(p->seed + (uint64_t)f);
+  ta.div_p = fast_div_make((unsigned)P);
   ta.tail_prio = !(p->flags & RT_FLAG_NO_TAIL_PRIORITY);
   ta.div_w = fast_div_make((unsigned)p->width);
   ta.work_counter = c->d_counters + kHeads;
@@ -757,7 +780,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
     ta.s_begin = s0;
     ta.s_count = sc;
     ta.div_s = fast_div_make((unsigned)sc);
-    ta.total_units = (uint64_t)P * sc;
+    ta.total_units = (uint64_t)nf * P * sc;
     queue_phases(ta, use_bvh ? c->grid_bvh : c->grid, use_bvh);
     HIP_TRY(hipEventRecord(c->ev[2 * ch], st));
     const double4* g4 = c->d_geo;
@@ -793,22 +816,29 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
       stamps ? pick(T{}, T{}, F{}, c->grid_bvh) : pick(T{}, F{}, F{}, c->grid_bvh);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[2 * ch + 1], st));
-    psrt::ReduceArgs ra{};
-    ra.samp_t = c->d_samples;
-    ra.samp_k = (const unsigned short*)(c->d_samples + P * sc);  // after the t array
-    ra.pixels = (unsigned)P;
-    ra.s_count = sc;
-    ra.first_chunk = ch == 0;
-    ra.spp_total = p->spp;
-    ra.accum = acc;
-    ra.rgb8 = (ch == nchunks - 1) ? d_rgb8 : nullptr;
-    ra.heads = c->d_counters + kHeads;
-    ra.sets = c->d_counters + kSets;
-    ra.totals = c->d_counters + kTotals;
-    ra.host_stats = (ch == nchunks - 1) ? c->d_stats : nullptr;
-    const unsigned blocks = (unsigned)((P + psrt::kReduceBlock - 1) / psrt::kReduceBlock);
-    hipLaunchKernelGGL(psrt::psrt_reduce, dim3(blocks), dim3(psrt::kReduceBlock), 0, st, ra);
-    HIP_TRY(hipGetLastError());
+    // one psrt_reduce per frame; frame 0's also folds the launch's counter
+    // sets into the render's totals and re-zeroes the queue heads
+    const size_t fu = P * (size_t)sc;  // units (records) of one frame in this chunk
+    for (size_t f = 0; f < nf; ++f) {
+      psrt::ReduceArgs ra{};
+      ra.samp_t = c->d_samples + f * fu;
+      // the k array follows the t array of all frames
+      ra.samp_k = (const unsigned short*)(c->d_samples + nf * fu) + f * fu;
+      ra.pixels = (unsigned)P;
+      ra.s_count = sc;
+      ra.first_chunk = ch == 0;
+      ra.spp_total = p->spp;
+      ra.accum = acc[f];
+      ra.rgb8 = (ch == nchunks - 1) ? rgb[f] : nullptr;
+      ra.fold_stats = f == 0;
+      ra.heads = c->d_counters + kHeads;
+      ra.sets = c->d_counters + kSets;
+      ra.totals = c->d_counters + kTotals;
+      ra.host_stats = (ch == nchunks - 1 && f == 0) ? c->d_stats : nullptr;
+      const unsigned blocks = (unsigned)((P + psrt::kReduceBlock - 1) / psrt::kReduceBlock);
+      hipLaunchKernelGGL(psrt::psrt_reduce, dim3(blocks), dim3(psrt::kReduceBlock), 0, st, ra);
+      HIP_TRY(hipGetLastError());
+    }
   }
   return RT_OK;
   };
@@ -822,7 +852,7 @@ int rt_render_device(rt_context* c, const rt_params* p, double* d_accum, unsigne
   c->dirty = false;
   c->ev_used = nchunks;
   c->last = rt_stats{};
-  c->last.samples = (uint64_t)P * p->spp;
+  c->last.samples = (uint64_t)nf * P * p->spp;
   c->n_last = c->n;
   return RT_OK;
 }

@@ -65,6 +65,10 @@ constexpr int kReduceTile = PSRT_REDUCE_TILE;  // samples per pixel per LDS tile
 constexpr size_t kSampleBytes = sizeof(double) + sizeof(unsigned short);
 
 
+// Frames of one multi-frame launch (rt_render_device_frames): the same shard
+// and scene, frame f with seed + f; the launch tail is paid once per batch.
+constexpr int kMaxFrames = 32;
+
 struct TraceArgs {
   int n;               // spheres (geo: {cx, cy, cz, r*r}, inv_r: 1.0/r)
   double org[3], llc[3], hor[3], ver[3];
@@ -72,8 +76,10 @@ struct TraceArgs {
   int row_offset, row_stride;
   unsigned pixels;      // rows_owned * width
   int s_begin, s_count; // sample chunk [s_begin, s_begin + s_count)
-  uint64_t total_units; // pixels * s_count  (< 2^32)
-  uint64_t seedmix;     // splitmix64(seed)
+  int frames;           // frames of this launch, 1..kMaxFrames: unit u = (f * pixels + q) *
+                        // s_count + s, frame f's records at [f * pixels * s_count, ...)
+  uint64_t total_units; // frames * pixels * s_count  (< 2^32)
+  uint64_t seedmix[kMaxFrames];  // splitmix64(seed + f) per frame f
   unsigned long long* work_counter;  // kQueues heads, kShardStride apart (one atomicAdd per ticket)
   // Guided work queue: tickets [ph_first[p], ph_first[p+1]) of phase p cover
   // ph_size[p] units each from unit ph_base[p] on; the last phase is open.
@@ -93,7 +99,7 @@ struct TraceArgs {
   int rng_extra;                    // extra trials while a scattering lane has none queued
   unsigned refill_min;              // idle lanes that trigger the finish + refill block
   unsigned walk_tail;               // a BVH pass stops once this few lanes still walk
-  FastDiv div_s, div_w;             // unit / s_count, q / width
+  FastDiv div_s, div_w, div_p;      // unit / s_count, q / width, (f * pixels + q) / pixels
   unsigned flush_at;                // per-lane counters flush to the totals at this value
   int tail_prio;                    // raise the issue priority of waves whose queue is empty
 };
@@ -153,6 +159,7 @@ struct ReduceArgs {
   int spp_total;
   double* accum;          // [pixels][3] (required unless single chunk + rgb only)
   unsigned char* rgb8;    // [pixels][3] or nullptr (last chunk only)
+  int fold_stats;         // block 0 folds the counter sets (one reduce per launch: frame 0's)
   // Statistics and queue state of the trace launch before this reduce
   // (block 0 only): the counter sets are added into totals (reset on the first
   // chunk), then the sets and the queue heads are zeroed for the next launch;

@@ -107,9 +107,9 @@ struct SectionClock {
 struct RefillConst {
   double cam[12];  // origin, lower_left, horizontal, vertical
   double wm1, hm1;  // (double)(W - 1), (double)(H - 1)   main.cc:80-81
-  uint64_t seedmix;
-  FastDiv div_s, div_w;
-  int hm1_i, row_offset, row_stride, s_begin;
+  uint64_t seedmix[kMaxFrames];  // splitmix64(seed of frame f) (TraceArgs::frames)
+  FastDiv div_s, div_w, div_p;
+  int hm1_i, row_offset, row_stride, s_begin, frames;
 };
 
 __device__ __forceinline__ unsigned fast_div(unsigned n, const FastDiv& f) {
@@ -800,12 +800,14 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
                             : threadIdx.x < 6 ? a.llc[threadIdx.x - 3]
                             : threadIdx.x < 9 ? a.hor[threadIdx.x - 6]
                                               : a.ver[threadIdx.x - 9];
+  if (threadIdx.x < kMaxFrames) s_rc.seedmix[threadIdx.x] = a.seedmix[threadIdx.x];
   if (threadIdx.x == 0) {
     s_rc.wm1 = (double)(a.width - 1);
     s_rc.hm1 = (double)(a.height - 1);
-    s_rc.seedmix = a.seedmix;
     s_rc.div_s = a.div_s;
     s_rc.div_w = a.div_w;
+    s_rc.div_p = a.div_p;
+    s_rc.frames = a.frames;
     s_rc.hm1_i = a.height - 1;
     s_rc.row_offset = a.row_offset;
     s_rc.row_stride = a.row_stride;
@@ -942,16 +944,21 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
           asm volatile("" : "+v"(zo));  // keeps the LDS reads below inside the loop
           const RefillConst& rc = *(const RefillConst*)((const char*)&s_rc + zo);
           const FastDiv ds = rc.div_s, dw = rc.div_w;
-          q = fast_div((unsigned)unit, ds);
+          q = fast_div((unsigned)unit, ds);  // f * pixels + pixel (frame-major units)
           su = (unsigned)unit;
           const unsigned sl = su - q * ds.d;
+          unsigned f = 0;  // frame of a multi-frame launch (wave-uniform branch)
+          if (rc.frames > 1) {
+            f = fast_div(q, rc.div_p);
+            q -= f * rc.div_p.d;
+          }
           const unsigned row_k = fast_div(q, dw);
           const unsigned i = q - row_k * dw.d;
           const int r = rc.row_offset + (int)row_k * rc.row_stride;
           const int j = rc.hm1_i - r;
           const unsigned pix = (unsigned)j * dw.d + i;
           const unsigned s = (unsigned)rc.s_begin + sl;
-          rng = splitmix64((((uint64_t)pix) << 32 | (uint64_t)s) ^ rc.seedmix);
+          rng = splitmix64((((uint64_t)pix) << 32 | (uint64_t)s) ^ rc.seedmix[f]);
           // main.cc:80-81, camera.h:25-28
           const double u = ((double)i + random_double(rng)) / rc.wm1;
           const double v = ((double)j + random_double(rng)) / rc.hm1;
@@ -1190,7 +1197,7 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
   // the trace launch's sharded counter sets -> totals (-> host), then the
   // sets and queue heads back to zero (ReduceArgs; stream order puts this
   // after every trace block and before the context's next launch)
-  if (blockIdx.x == 0) {
+  if (blockIdx.x == 0 && a.fold_stats) {
     if (threadIdx.x < 4) {
       unsigned long long v = a.first_chunk ? 0ull : a.totals[threadIdx.x];
       for (int h = 0; h < kQueues; ++h) {

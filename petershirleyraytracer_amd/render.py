@@ -216,6 +216,21 @@ class Context:
         check(self._L.rt_render_device(self.handle, C.byref(p), d_accum or None,
                                        d_rgb8 or None, stream or None), "rt_render_device")
 
+    def render_device_frames(self, p: RtParams, nframes: int, d_accum=None, d_rgb8=None,
+                             stream: int = 0) -> None:
+        """Enqueue nframes renders in one trace launch per sample chunk: frame f
+        is the frame of seed p.seed + f; d_accum / d_rgb8: sequences of nframes
+        device pointers (ints, 0 = none) or None."""
+        def arr(ptrs):
+            if ptrs is None:
+                return None
+            if len(ptrs) != nframes:
+                raise ValueError("one pointer per frame")
+            return (C.c_void_p * nframes)(*[x or None for x in ptrs])
+        check(self._L.rt_render_device_frames(self.handle, C.byref(p), nframes, arr(d_accum),
+                                              arr(d_rgb8), stream or None),
+              "rt_render_device_frames")
+
     def stream(self) -> int:
         """The context's own hipStream_t (as an int), used for stream=0."""
         return self._L.rt_context_stream(self.handle) or 0

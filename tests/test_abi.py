@@ -36,7 +36,7 @@ def test_exports_every_declared_symbol():
 
 def test_abi_version_and_info():
     L = _lib.load()
-    assert L.rt_abi_version() == 3
+    assert L.rt_abi_version() == 4
     assert b"gfx950" in L.rt_build_info()
 
 

@@ -162,3 +162,44 @@ def test_render_into_pinned_host_memory():
         assert np.array_equal(host.numpy(), rgb), (w, h)
         del host
         ctx.close()
+
+
+@pytest.mark.parametrize("buf_mb", [None, "1"])
+def test_multi_frame_launch_equals_single_frames(monkeypatch, buf_mb):
+    """rt_render_device_frames: frame f of a batch is bit for bit the frame of
+    seed + f rendered alone (per-frame seeds, frame-major units, one stats
+    fold), for a shard of the final scene, in one sample chunk and (1 MB
+    buffer) in several chunks whose running sums continue per frame."""
+    import torch
+    sph = P.scene_random_spheres(1)
+    w, h, spp, nf = 64, 40, 12, 5
+    cam = P.camera_look_at(aspect=w / h)
+    rows = P.rows_owned(h, 1, 3)
+    if buf_mb:
+        monkeypatch.setenv("PSRT_SAMPLE_BUF_MB", buf_mb)
+    ctx = P.Context(0)
+    ctx.set_scene(sph, cam)
+    acc = torch.zeros((nf, rows, w, 3), dtype=torch.float64, device="cuda:0")
+    rgb = torch.zeros((nf, rows, w, 3), dtype=torch.uint8, device="cuda:0")
+    prm = P.params(w, h, spp, 50, 7, 1, 3)
+    ctx.render_device_frames(prm, nf, [acc[f].data_ptr() for f in range(nf)],
+                             [rgb[f].data_ptr() for f in range(nf)])
+    st = ctx.sync_stats()
+    torch.cuda.synchronize()
+    rays = 0
+    for f in range(nf):
+        want, wrgb, ws = P.render(sph, cam, w, h, spp, 50, 7 + f, row_offset=1, row_stride=3)
+        assert np.array_equal(bits(acc[f].cpu().numpy()), bits(want)), f
+        assert np.array_equal(rgb[f].cpu().numpy(), wrgb), f
+        rays += ws["rays"]
+    assert st["rays"] == rays and st["samples"] == nf * rows * w * spp
+    # a NULL entry (frame 2 without bytes) and no accumulator array
+    ctx.render_device_frames(prm, 3, None, [rgb[0].data_ptr(), 0, rgb[1].data_ptr()])
+    ctx.sync_stats()
+    torch.cuda.synchronize()
+    _, r0, _ = P.render(sph, cam, w, h, spp, 50, 7, row_offset=1, row_stride=3)
+    _, r2, _ = P.render(sph, cam, w, h, spp, 50, 9, row_offset=1, row_stride=3)
+    assert np.array_equal(rgb[0].cpu().numpy(), r0) and np.array_equal(rgb[1].cpu().numpy(), r2)
+    with pytest.raises(RuntimeError):
+        ctx.render_device_frames(prm, 33)
+    ctx.close()
