@@ -26,5 +26,5 @@ for l in lines:
     if m:
         cur = "%s:%s" % (files.get(int(m.group(1)), "?").split("/")[-1], m.group(2))
         continue
-    if re.match(r"\s+[vs]_", l) or re.match(r"^\.LBB", l):
+    if re.match(r"\s+(v|s|ds|global|buffer|scratch)_", l) or re.match(r"^\.LBB", l):
         print("%-24s %s" % (cur, l.strip()[:110]))
