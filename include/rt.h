@@ -90,6 +90,10 @@ typedef struct {
  * box_tests) with a slower kernel variant (~1%); without it both read 0.
  * Same bits; every other counter is always exact. */
 #define RT_FLAG_CULL_STATS 8u
+/* render with the material integrator and lens camera of the context
+ * (rt_context_set_materials) instead of the reference's
+ * diffuse ray_color */
+#define RT_FLAG_MATERIALS 16u
 
 typedef struct {
   int width;      /* image_width  (main.cc:57)                              */
@@ -202,6 +206,70 @@ int rt_scene_two_spheres(rt_sphere* out, int cap);
  * stream, ground r=1000, 22x22 jittered r=0.2 grid, three r=1 spheres,
  * diffuse-only. Returns the sphere count; writes at most cap records. */
 int rt_scene_random_spheres(unsigned int seed, rt_sphere* out, int cap);
+
+/* ---- materials and defocus (extension: SURVEY.md §8(f)4; parity unpinned) ---
+ * The reference traces one material, 0.5-attenuation hemisphere diffuse
+ * (main.cc:42-43), through a fixed pinhole (camera.h:11-23). The book it
+ * follows (Ray Tracing in One Weekend v3.2, ch. 9-13) goes on to materials
+ * and a thin-lens camera; this is that integrator, restated:
+ *   ray_color: depth <= 0 -> black; world.hit(r, 0.001, inf); on a hit the
+ *     material scatters (attenuation * ray_color(scattered, depth - 1), the
+ *     product taken innermost first, as the recursion does) or absorbs
+ *     (black); a miss returns the sky of main.cc:46-48.
+ *   lambertian: normal + random_unit_vector() (vec3.h:97-100), the normal when
+ *     that is near zero (all |e| < 1e-8); metal: reflect(unit(d), n) +
+ *     fuzz * random_in_unit_sphere(), absorbed unless dot(scattered, n) > 0;
+ *   dielectric: Snell / Schlick (pow(x, 5) evaluated as (x*x)*(x*x)*x), one
+ *     random_double() drawn only when refraction is possible.
+ *   thin lens: get_ray(s, t) offsets the origin by lens_radius *
+ *     random_in_unit_disk() (g++ draw order: y then x) along u, v.
+ * No reference output exists for any of this: tests check the device
+ * against a CPU restatement of it bit for bit ("parity unpinned"). */
+#define RT_MAT_LAMBERTIAN 0
+#define RT_MAT_METAL 1
+#define RT_MAT_DIELECTRIC 2
+
+/* One material per sphere, same index as the sphere list. */
+typedef struct {
+  int kind;          /* RT_MAT_*                                      */
+  int reserved;      /* 0                                             */
+  double albedo[3];  /* lambertian / metal attenuation                */
+  double fuzz;       /* metal: reflection fuzz (book clamps to <= 1)  */
+  double ir;         /* dielectric: index of refraction               */
+} rt_material;
+
+/* The thin-lens camera: the pinhole basis plus the lens frame. */
+typedef struct {
+  rt_camera base;     /* origin, lower_left, horizontal, vertical (focus plane) */
+  double u[3], v[3];  /* unit lens axes (camera right / up)                     */
+  double lens_radius; /* aperture / 2 (0: a pinhole, no lens draws)             */
+} rt_camera_lens;
+
+/* camera(lookfrom, lookat, vup, vfov, aspect, aperture, focus_dist) of the
+ * book (ch. 12); with aperture 0 and focus_dist 1 its base equals
+ * rt_camera_look_at. */
+int rt_camera_look_at_lens(const double lookfrom[3], const double lookat[3],
+                           const double vup[3], double vfov_deg, double aspect,
+                           double aperture, double focus_dist, rt_camera_lens* out);
+
+/* The book's random_scene() (ch. 13) on the glibc srand(seed) stream, with
+ * g++'s argument evaluation order for every vec3 built from draws: ground
+ * (lambertian 0.5), 22x22 jittered r = 0.2 spheres (80% lambertian with
+ * albedo random()*random(), 15% metal, 5% glass 1.5), glass / lambertian /
+ * metal r = 1 spheres. Returns the sphere count; writes at most cap records
+ * into out and mats (either may be NULL). */
+int rt_scene_book_final(unsigned int seed, rt_sphere* out, rt_material* mats, int cap);
+
+/* Materials (one per sphere of the context's scene, same order) and the lens
+ * camera for renders with RT_FLAG_MATERIALS. n must equal the scene's count.
+ * mats == NULL clears them. */
+int rt_context_set_materials(rt_context* ctx, const rt_material* mats, int n,
+                             const rt_camera_lens* cam);
+
+/* One-shot material render (rt_render with RT_FLAG_MATERIALS): host buffers. */
+int rt_render_materials(const rt_sphere* spheres, const rt_material* mats, int n_spheres,
+                        const rt_camera_lens* cam, const rt_params* params,
+                        double* accum_rgb, unsigned char* rgb8, rt_stats* stats);
 
 /* ---- scene files (extension: SURVEY.md §8(f)3) ------------------------------
  * Text form of main.cc:53-63 (spheres in hittable_list order, camera,

@@ -52,6 +52,16 @@ class Params(C.Structure):
     ]
 
 
+class Material(C.Structure):
+    _fields_ = [("kind", C.c_int), ("reserved", C.c_int), ("albedo", C.c_double * 3),
+                ("fuzz", C.c_double), ("ir", C.c_double)]
+
+
+class CameraLens(C.Structure):
+    _fields_ = [("base", Camera), ("u", C.c_double * 3), ("v", C.c_double * 3),
+                ("lens_radius", C.c_double)]
+
+
 class Bounce(C.Structure):
     _fields_ = [
         ("o", C.c_double * 3),
@@ -107,6 +117,15 @@ def lib():
         L.oracle_quantize.argtypes = [C.POINTER(C.c_double), C.c_int, C.c_int, C.c_int,
                                       C.POINTER(C.c_ubyte)]
         L.oracle_rows_owned.argtypes = [C.c_int, C.c_int, C.c_int]
+        # rt_oracle_mat.c (materials extension, parity unpinned)
+        L.oracle_render_mat.argtypes = [
+            C.POINTER(Sphere), C.POINTER(Material), C.c_int, C.POINTER(CameraLens),
+            C.POINTER(Params), C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
+        L.oracle_scene_book_final.argtypes = [C.c_uint, C.POINTER(Sphere), C.POINTER(Material),
+                                              C.c_int]
+        L.oracle_camera_look_at_lens.argtypes = [C.POINTER(C.c_double)] * 3 + [
+            C.c_double] * 4 + [C.POINTER(CameraLens)]
+        L.oracle_camera_look_at_lens.restype = None
         _lib = L
     return _lib
 
@@ -278,3 +297,68 @@ def run_ref(args: Sequence[str], timeout: Optional[float] = None):
         if line.startswith("{"):
             stats = json.loads(line)
     return r.stdout, stats
+
+
+# ---- materials extension (rt_oracle_mat.c; DESIGN.md §14, parity unpinned) ----
+
+def materials_struct(mats):
+    """mats: (n, 6) rows (kind, albedo r, g, b, fuzz, ir)."""
+    a = np.asarray(mats, dtype=np.float64).reshape(-1, 6)
+    out = (Material * max(1, len(a)))()
+    for k, row in enumerate(a):
+        out[k].kind = int(row[0])
+        out[k].albedo[0], out[k].albedo[1], out[k].albedo[2] = row[1], row[2], row[3]
+        out[k].fuzz, out[k].ir = row[4], row[5]
+    return out, len(a)
+
+
+def lens_to_dict(c: CameraLens) -> dict:
+    return dict(base=camera_to_array(c.base), u=np.array(list(c.u)), v=np.array(list(c.v)),
+                lens_radius=c.lens_radius)
+
+
+def lens_from(base, u, v, lens_radius) -> CameraLens:
+    c = CameraLens()
+    c.base = camera_from_array(base)
+    for k in range(3):
+        c.u[k], c.v[k] = float(u[k]), float(v[k])
+    c.lens_radius = float(lens_radius)
+    return c
+
+
+def camera_look_at_lens(lookfrom=(13, 2, 3), lookat=(0, 0, 0), vup=(0, 1, 0), vfov=20.0,
+                        aspect=1.5, aperture=0.1, focus_dist=10.0) -> dict:
+    c = CameraLens()
+    d3 = C.c_double * 3
+    lib().oracle_camera_look_at_lens(d3(*lookfrom), d3(*lookat), d3(*vup), vfov, aspect,
+                                     aperture, focus_dist, C.byref(c))
+    return lens_to_dict(c)
+
+
+def scene_book_final(seed: int = 1):
+    sp = (Sphere * 1024)()
+    mt = (Material * 1024)()
+    n = lib().oracle_scene_book_final(seed, sp, mt, 1024)
+    spheres = np.frombuffer(sp, dtype=np.float64, count=n * 4).reshape(n, 4).copy()
+    mats = np.array([[mt[k].kind, *list(mt[k].albedo), mt[k].fuzz, mt[k].ir] for k in range(n)],
+                    dtype=np.float64).reshape(n, 6)
+    return spheres, mats
+
+
+def render_mat(spheres, mats, lens: dict, width, height, spp, max_depth=50, seed=0,
+               row_offset=0, row_stride=1, threads=1):
+    """The book's material integrator over the counter stream.
+    Returns (accum[rows, W, 3] float64, rays)."""
+    sp, n = spheres_array(spheres)
+    mt, nm = materials_struct(mats)
+    assert nm == n
+    cam = lens_from(lens["base"], lens["u"], lens["v"], lens["lens_radius"])
+    p = make_params(width, height, spp, max_depth, seed, row_offset, row_stride)
+    rows = rows_owned(height, row_offset, row_stride)
+    acc = np.zeros((rows, width, 3), dtype=np.float64)
+    rays = C.c_uint64(0)
+    rc = lib().oracle_render_mat(sp, mt, n, C.byref(cam), C.byref(p), threads,
+                                 acc.ctypes.data_as(C.POINTER(C.c_double)), C.byref(rays))
+    if rc != 0:
+        raise RuntimeError(f"oracle_render_mat failed: {rc}")
+    return acc, rays.value

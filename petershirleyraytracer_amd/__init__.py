@@ -6,13 +6,15 @@ This Python package is host plumbing over that C ABI: scene/camera helpers,
 one-shot and device-resident renders, PPM output, and the multi-GPU sharding
 used by ``bench.py``. See DESIGN.md.
 """
-from .render import (Context, SceneFile, camera_default, camera_look_at, device_count,
-                     format_scene, load_scene, params, parse_scene, ppm_p3, probe_f64, quantize,
-                     render, rows_owned, save_scene, scene_random_spheres, scene_two_spheres,
-                     write_ppm)
+from .render import (Context, LensCamera, SceneFile, camera_default, camera_look_at,
+                     camera_look_at_lens, device_count, format_scene, load_scene, params,
+                     parse_scene, ppm_p3, probe_f64, quantize, render, render_materials,
+                     rows_owned, save_scene, scene_book_final, scene_random_spheres,
+                     scene_two_spheres, write_ppm)
 
 __all__ = [
-    "Context", "SceneFile", "camera_default", "camera_look_at", "device_count", "format_scene",
-    "load_scene", "params", "parse_scene", "ppm_p3", "probe_f64", "quantize", "render",
-    "rows_owned", "save_scene", "scene_random_spheres", "scene_two_spheres", "write_ppm",
+    "Context", "LensCamera", "SceneFile", "camera_default", "camera_look_at",
+    "camera_look_at_lens", "device_count", "format_scene", "load_scene", "params", "parse_scene",
+    "ppm_p3", "probe_f64", "quantize", "render", "render_materials", "rows_owned", "save_scene",
+    "scene_book_final", "scene_random_spheres", "scene_two_spheres", "write_ppm",
 ]

@@ -22,6 +22,8 @@ EXPORTS = [
     "rt_scene_parse", "rt_scene_load", "rt_scene_format",
     "rt_last_error", "rt_abi_version", "rt_device_count", "rt_build_info", "rt_debug_probe_f64",
     "rt_debug_world_hit", "rt_debug_world_hit_hint",
+    "rt_camera_look_at_lens", "rt_scene_book_final", "rt_context_set_materials",
+    "rt_render_materials",
 ]
 
 
@@ -38,6 +40,16 @@ class RtParams(C.Structure):
     _fields_ = [("width", C.c_int), ("height", C.c_int), ("spp", C.c_int),
                 ("max_depth", C.c_int), ("seed", C.c_uint64), ("row_offset", C.c_int),
                 ("row_stride", C.c_int), ("flags", C.c_uint)]
+
+
+class RtMaterial(C.Structure):
+    _fields_ = [("kind", C.c_int), ("reserved", C.c_int), ("albedo", C.c_double * 3),
+                ("fuzz", C.c_double), ("ir", C.c_double)]
+
+
+class RtCameraLens(C.Structure):
+    _fields_ = [("base", RtCamera), ("u", C.c_double * 3), ("v", C.c_double * 3),
+                ("lens_radius", C.c_double)]
 
 
 class RtStats(C.Structure):
@@ -113,6 +125,14 @@ def load(build_if_missing: bool = False):
                                 C.c_int], C.c_int),
         "rt_debug_world_hit_hint": ([P(RtSphere), C.c_int, P(C.c_double), P(C.c_int), C.c_int,
                                      P(C.c_double), C.c_int], C.c_int),
+        "rt_camera_look_at_lens": ([P(C.c_double), P(C.c_double), P(C.c_double), C.c_double,
+                                    C.c_double, C.c_double, C.c_double, P(RtCameraLens)],
+                                   C.c_int),
+        "rt_scene_book_final": ([C.c_uint, P(RtSphere), P(RtMaterial), C.c_int], C.c_int),
+        "rt_context_set_materials": ([C.c_void_p, P(RtMaterial), C.c_int, P(RtCameraLens)],
+                                     C.c_int),
+        "rt_render_materials": ([P(RtSphere), P(RtMaterial), C.c_int, P(RtCameraLens),
+                                 P(RtParams), P(C.c_double), P(C.c_ubyte), P(RtStats)], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -153,6 +153,14 @@ struct rt_context {
   // a render failed after its first trace launch: queue heads / counter sets
   // may be non-zero until the next render re-zeroes them (stream-ordered)
   bool dirty = false;
+  // material integrator (rt_context_set_materials)
+  int grid_mat = 0, grid_mat_bvh = 0;  // resident blocks of psrt_trace_mat<false / true>
+  bool has_mats = false;               // materials set for the current scene
+  psrt::DevMaterial* d_mats = nullptr;
+  int mats_cap = 0;
+  rt_camera_lens lcam{};
+  int* d_path = nullptr;  // per resident lane, its path's attenuating hits
+  size_t path_cap = 0;    // ints
   rt_stats last{};
   int n_last = 0;
 };
@@ -273,6 +281,12 @@ int rt_context_create(int device, rt_context** out) {
       break;
     }
   }
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace_mat<false>,
+                                                        psrt::kMatBlock, 0));
+  c->grid_mat = c->cus * (per_cu < 1 ? 1 : per_cu);
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace_mat<true>,
+                                                        psrt::kMatBlock, 0));
+  c->grid_mat_bvh = c->cus * (per_cu < 1 ? 1 : per_cu);
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIP_TRY(hipMalloc(&c->d_counters, kCounterWords * sizeof(unsigned long long)));
   // zeroed once: psrt_reduce leaves the queue heads and counter sets at zero
@@ -309,6 +323,8 @@ int rt_context_destroy(rt_context* c) {
   (void)hipFree(c->d_cell_items);
   (void)hipFree(c->d_nb_word);
   (void)hipFree(c->d_nb_items);
+  (void)hipFree(c->d_mats);
+  (void)hipFree(c->d_path);
   for (auto e : c->ev) (void)hipEventDestroy(e);
   if (c->ev_all0) (void)hipEventDestroy(c->ev_all0);
   if (c->ev_all1) (void)hipEventDestroy(c->ev_all1);
@@ -336,6 +352,7 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
     return RT_OK;
   }
   c->scene.clear();  // set again once every structure is built
+  c->has_mats = false;  // materials belong to the scene they were set for
   const int cap = n > 0 ? n : 1;
   if (cap > c->n_cap) {
     (void)hipFree(c->d_geo);
@@ -474,9 +491,12 @@ static int check_params(const rt_params* p) {
                 p->row_stride, p->height);
   if ((long long)p->width * p->height >= (1LL << 32))
     return set_error(RT_E_INVALID, "image too large for 32-bit pixel ids");
-  if (p->flags &
-      ~(RT_FLAG_NO_CULL | RT_FLAG_NO_FIXPOINT | RT_FLAG_NO_TAIL_PRIORITY | RT_FLAG_CULL_STATS))
+  if (p->flags & ~(RT_FLAG_NO_CULL | RT_FLAG_NO_FIXPOINT | RT_FLAG_NO_TAIL_PRIORITY |
+                   RT_FLAG_CULL_STATS | RT_FLAG_MATERIALS))
     return set_error(RT_E_INVALID, "unknown flags 0x%x", p->flags);
+  if ((p->flags & RT_FLAG_MATERIALS) && p->max_depth > psrt::kMatMaxDepth)
+    return set_error(RT_E_INVALID, "max_depth %d above %d with RT_FLAG_MATERIALS", p->max_depth,
+                     psrt::kMatMaxDepth);
   return RT_OK;
 }
 
@@ -547,6 +567,12 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
                      psrt::kMaxFrames);
   const size_t nf = (size_t)nframes;  // frames of the batch
   if (c->n < 0) return set_error(RT_E_SCENE, "rt_render_device: no scene set");
+  // RT_FLAG_MATERIALS: the material integrator (psrt_mat.hip) over the
+  // context's materials and lens camera; colour records of 3 doubles
+  const bool mat = (p->flags & RT_FLAG_MATERIALS) != 0;
+  if (mat && !c->has_mats)
+    return set_error(RT_E_SCENE, "RT_FLAG_MATERIALS: no materials set for this scene");
+  const size_t rec_bytes = mat ? psrt::kMatSampleBytes : psrt::kSampleBytes;
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = stream_ ? (hipStream_t)stream_ : c->stream;
   const int rows = rt_rows_owned(p->height, p->row_offset, p->row_stride);
@@ -603,13 +629,13 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     }
     return sc;
   };
-  size_t s_chunk = plan(cap_bytes / (nf * P * psrt::kSampleBytes));
+  size_t s_chunk = plan(cap_bytes / (nf * P * rec_bytes));
   // t array (doubles) then k array (uint16), P x s_chunk records each. If the
   // allocation still fails (another process took the memory meanwhile), halve
   // the chunk and try again.
   for (;;) {
     const size_t recs = nf * P * s_chunk;
-    rc = ensure_buf(c, &c->d_samples, &c->samples_cap, recs + (recs + 3) / 4);
+    rc = ensure_buf(c, &c->d_samples, &c->samples_cap, mat ? 3 * recs : recs + (recs + 3) / 4);
     if (rc == RT_E_NOMEM && s_chunk > 1) {
       (void)hipGetLastError();  // clear the failed hipMalloc
       s_chunk = plan(s_chunk / 2);
@@ -637,6 +663,46 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
   }
   rc = ensure_events(c, nchunks);
   if (rc) return rc;
+  const bool use_bvh = c->bvh && !(p->flags & RT_FLAG_NO_CULL);
+  psrt::MatArgs ma{};
+  if (mat) {  // the path scratch: one column per resident lane, max_depth rows
+    const size_t lanes = (size_t)(use_bvh ? c->grid_mat_bvh : c->grid_mat) * psrt::kMatBlock;
+    const size_t need_ints = lanes * (size_t)std::max(1, p->max_depth);
+    if (c->path_cap < need_ints) {
+      rc = quiesce(c);
+      if (rc) return rc;
+      (void)hipFree(c->d_path);
+      c->d_path = nullptr;
+      c->path_cap = 0;
+      HIP_TRY(hipMalloc(&c->d_path, need_ints * sizeof(int)));
+      c->path_cap = need_ints;
+    }
+    ma.n = c->n;
+    for (int k = 0; k < 3; ++k) {
+      ma.org[k] = c->lcam.base.origin[k];
+      ma.llc[k] = c->lcam.base.lower_left[k];
+      ma.hor[k] = c->lcam.base.horizontal[k];
+      ma.ver[k] = c->lcam.base.vertical[k];
+      ma.lu[k] = c->lcam.u[k];
+      ma.lv[k] = c->lcam.v[k];
+    }
+    ma.lens_radius = c->lcam.lens_radius;
+    ma.width = p->width;
+    ma.height = p->height;
+    ma.max_depth = p->max_depth;
+    ma.row_offset = p->row_offset;
+    ma.row_stride = p->row_stride;
+    ma.pixels = (unsigned)P;
+    ma.frames = nframes;
+    for (int f = 0; f < nframes; ++f) ma.seedmix[f] = splitmix64_host(p->seed + (uint64_t)f);
+    ma.div_p = fast_div_make((unsigned)P);
+    ma.div_w = fast_div_make((unsigned)p->width);
+    ma.work_counter = c->d_counters + kHeads;
+    ma.ray_counter = c->d_counters + kSets;
+    ma.mats = c->d_mats;
+    ma.path = c->d_path;
+    ma.path_stride = (unsigned)lanes;
+  }
 
   psrt::TraceArgs ta{};
   ta.n = c->n;
@@ -663,7 +729,7 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
   // No memset here: the queue heads and counter sets are zero (context
   // creation, then every psrt_reduce), and a small fill kernel on this stream
   // would wait for a CU slot behind another frame's persistent launch.
-  const bool stamps = std::getenv("PSRT_STAMPS") != nullptr;  // diagnostic build
+  const bool stamps = !mat && std::getenv("PSRT_STAMPS") != nullptr;  // diagnostic build
   if (stamps) HIP_TRY(hipMemsetAsync(c->d_counters + 8, 0, 120 * sizeof(unsigned long long), st));
   ta.stamps = c->d_counters + 8;
   ta.wave_log = nullptr;
@@ -712,14 +778,13 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
       if (v >= 1 && v < ta.flush_at) ta.flush_at = (unsigned)v;
     }
   }
-  const bool use_bvh = c->bvh && !(p->flags & RT_FLAG_NO_CULL);
   psrt::BvhView bv = bvh_view(c);
   bv.fixpoint = !(p->flags & RT_FLAG_NO_FIXPOINT) && !std::getenv("PSRT_NO_FIXPOINT");
   // camera-ray candidate lists: BVH scenes whose indices fit uint16 and whose
   // camera lies inside the range the pad covers (|o|_inf <= r_check)
   const double om = std::max(std::fabs(c->cam.origin[0]),
                              std::max(std::fabs(c->cam.origin[1]), std::fabs(c->cam.origin[2])));
-  const bool camlist = use_bvh && c->n < (int)psrt::kCamOverflow && om <= c->r_check &&
+  const bool camlist = !mat && use_bvh && c->n < (int)psrt::kCamOverflow && om <= c->r_check &&
                        !std::getenv("PSRT_NO_CAMLIST");
   if (camlist && c->plist_cap < P) {
     rc = quiesce(c);
@@ -781,6 +846,43 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     ta.s_count = sc;
     ta.div_s = fast_div_make((unsigned)sc);
     ta.total_units = (uint64_t)nf * P * sc;
+    const size_t fu = P * (size_t)sc;  // units (records) of one frame in this chunk
+    if (mat) {
+      ma.s_begin = s0;
+      ma.s_count = sc;
+      ma.div_s = ta.div_s;
+      ma.total_units = ta.total_units;
+      HIP_TRY(hipEventRecord(c->ev[2 * ch], st));
+      const int grid = use_bvh ? c->grid_mat_bvh : c->grid_mat;
+      if (use_bvh)
+        hipLaunchKernelGGL(psrt::psrt_trace_mat<true>, dim3(grid), dim3(psrt::kMatBlock), 0, st,
+                           c->d_geo, c->d_inv_r, c->d_samples, ma, bv);
+      else
+        hipLaunchKernelGGL(psrt::psrt_trace_mat<false>, dim3(grid), dim3(psrt::kMatBlock), 0, st,
+                           c->d_geo, c->d_inv_r, c->d_samples, ma, bv);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipEventRecord(c->ev[2 * ch + 1], st));
+      for (size_t f = 0; f < nf; ++f) {
+        psrt::ReduceArgs ra{};
+        ra.samp_t = c->d_samples + 3 * f * fu;
+        ra.pixels = (unsigned)P;
+        ra.s_count = sc;
+        ra.first_chunk = ch == 0;
+        ra.spp_total = p->spp;
+        ra.accum = acc[f];
+        ra.rgb8 = (ch == nchunks - 1) ? rgb[f] : nullptr;
+        ra.fold_stats = f == 0;
+        ra.heads = c->d_counters + kHeads;
+        ra.sets = c->d_counters + kSets;
+        ra.totals = c->d_counters + kTotals;
+        ra.host_stats = (ch == nchunks - 1 && f == 0) ? c->d_stats : nullptr;
+        const unsigned blocks = (unsigned)((P + psrt::kReduceBlock - 1) / psrt::kReduceBlock);
+        hipLaunchKernelGGL(psrt::psrt_reduce_rgb, dim3(blocks), dim3(psrt::kReduceBlock), 0, st,
+                           ra);
+        HIP_TRY(hipGetLastError());
+      }
+      continue;
+    }
     queue_phases(ta, use_bvh ? c->grid_bvh : c->grid, use_bvh);
     HIP_TRY(hipEventRecord(c->ev[2 * ch], st));
     const double4* g4 = c->d_geo;
@@ -818,7 +920,6 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     HIP_TRY(hipEventRecord(c->ev[2 * ch + 1], st));
     // one psrt_reduce per frame; frame 0's also folds the launch's counter
     // sets into the render's totals and re-zeroes the queue heads
-    const size_t fu = P * (size_t)sc;  // units (records) of one frame in this chunk
     for (size_t f = 0; f < nf; ++f) {
       psrt::ReduceArgs ra{};
       ra.samp_t = c->d_samples + f * fu;
@@ -1012,6 +1113,86 @@ int rt_render(const rt_sphere* sph, int n, const rt_camera* cam, const rt_params
   double* d_acc = c->d_accum_tmp;
   unsigned char* d_rgb = (unsigned char*)(c->d_accum_tmp + P * 3);
   rc = rt_render_device(c, p, d_acc, rgb8 ? d_rgb : nullptr, nullptr);
+  if (rc) return rc;
+  rc = rt_context_sync_stats(c, stats);
+  if (rc) return rc;
+  if (accum_rgb && P)
+    HIP_TRY(hipMemcpy(accum_rgb, d_acc, P * 3 * sizeof(double), hipMemcpyDeviceToHost));
+  if (rgb8 && P) HIP_TRY(hipMemcpy(rgb8, d_rgb, P * 3, hipMemcpyDeviceToHost));
+  return RT_OK;
+}
+
+int rt_context_set_materials(rt_context* c, const rt_material* mats, int n,
+                             const rt_camera_lens* cam) {
+  if (!c) return set_error(RT_E_INVALID, "rt_context_set_materials: ctx is NULL");
+  if (!mats) {
+    c->has_mats = false;
+    return RT_OK;
+  }
+  if (!cam) return set_error(RT_E_INVALID, "rt_context_set_materials: cam is NULL");
+  if (c->n < 0) return set_error(RT_E_SCENE, "rt_context_set_materials: no scene set");
+  if (n != c->n)
+    return set_error(RT_E_INVALID, "rt_context_set_materials: %d materials for %d spheres", n, c->n);
+  std::vector<psrt::DevMaterial> dm((size_t)std::max(1, n));
+  for (int k = 0; k < n; ++k) {
+    const rt_material& m = mats[k];
+    if (m.kind != RT_MAT_LAMBERTIAN && m.kind != RT_MAT_METAL && m.kind != RT_MAT_DIELECTRIC)
+      return set_error(RT_E_INVALID, "rt_context_set_materials: material %d has kind %d", k, m.kind);
+    psrt::DevMaterial& d = dm[k];
+    d = psrt::DevMaterial{};
+    for (int ch = 0; ch < 3; ++ch) d.albedo[ch] = m.albedo[ch];
+    d.fuzz = m.fuzz < 1 ? m.fuzz : 1;  // metal(a, f): fuzz(f < 1 ? f : 1)
+    d.ir = m.ir;
+    d.kind = m.kind;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  {  // the last render may still read the materials
+    const int rc = quiesce(c);
+    if (rc) return rc;
+  }
+  if (n > c->mats_cap) {
+    (void)hipFree(c->d_mats);
+    c->d_mats = nullptr;
+    c->mats_cap = 0;
+    HIP_TRY(hipMalloc(&c->d_mats, (size_t)n * sizeof(psrt::DevMaterial)));
+    c->mats_cap = n;
+  }
+  if (n > 0) {
+    HIP_TRY(hipMemcpyAsync(c->d_mats, dm.data(), (size_t)n * sizeof(psrt::DevMaterial),
+                           hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  }
+  c->lcam = *cam;
+  c->has_mats = true;
+  return RT_OK;
+}
+
+int rt_render_materials(const rt_sphere* sph, const rt_material* mats, int n,
+                        const rt_camera_lens* cam, const rt_params* p, double* accum_rgb,
+                        unsigned char* rgb8, rt_stats* stats) {
+  if (!cam || !p || !mats || n < 0 || (n > 0 && !sph))
+    return set_error(RT_E_INVALID, "rt_render_materials: bad arguments");
+  rt_params q = *p;
+  q.flags |= RT_FLAG_MATERIALS;
+  int rc = check_params(&q);
+  if (rc) return rc;
+  if (!accum_rgb && !rgb8 && rt_rows_owned(q.height, q.row_offset, q.row_stride) > 0)
+    return set_error(RT_E_INVALID, "rt_render_materials: no output buffer");
+  rt_context* c = nullptr;
+  std::unique_lock<std::mutex> lk;
+  rc = get_default_context(&c, &lk);
+  if (rc) return rc;
+  rc = rt_context_set_scene(c, sph, n, &cam->base);
+  if (rc) return rc;
+  rc = rt_context_set_materials(c, mats, n, cam);
+  if (rc) return rc;
+  const int rows = rt_rows_owned(q.height, q.row_offset, q.row_stride);
+  const size_t P = (size_t)rows * q.width;
+  rc = ensure_buf(c, &c->d_accum_tmp, &c->accum_tmp_cap, P * 3 + (P * 3 + 7) / 8 + 1);
+  if (rc) return rc;
+  double* d_acc = c->d_accum_tmp;
+  unsigned char* d_rgb = (unsigned char*)(c->d_accum_tmp + P * 3);
+  rc = rt_render_device(c, &q, d_acc, rgb8 ? d_rgb : nullptr, nullptr);
   if (rc) return rc;
   rc = rt_context_sync_stats(c, stats);
   if (rc) return rc;

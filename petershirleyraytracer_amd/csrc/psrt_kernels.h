@@ -170,6 +170,49 @@ struct ReduceArgs {
   unsigned long long* host_stats;  // [4], or nullptr
 };
 
+// ---- material integrator (psrt_mat.hip) ----
+// One material per sphere (rt_material, fuzz clamped to <= 1 by the host).
+struct DevMaterial {
+  double albedo[3];
+  double fuzz;
+  double ir;
+  int kind;  // RT_MAT_*
+  int pad_;
+};
+static_assert(sizeof(DevMaterial) == 48, "device material layout");
+constexpr int kMatBlock = 256;
+constexpr unsigned kMatChunk = 256;  // units per queue ticket
+constexpr int kMatMaxDepth = 4096;   // path scratch rows (max_depth bound of RT_FLAG_MATERIALS)
+// Sample record of the material path: the sample's colour, 3 doubles, in unit
+// order (unit u = (f * pixels + q) * s_count + s, as TraceArgs).
+constexpr size_t kMatSampleBytes = 3 * sizeof(double);
+
+struct MatArgs {
+  int n;
+  double org[3], llc[3], hor[3], ver[3];  // focus-plane basis (camera get_ray)
+  double lu[3], lv[3], lens_radius;       // thin lens: offset = lu rd.x + lv rd.y
+  int width, height, max_depth;
+  int row_offset, row_stride;
+  unsigned pixels;
+  int s_begin, s_count, frames;
+  uint64_t total_units;  // frames * pixels * s_count (< 2^32)
+  uint64_t seedmix[kMaxFrames];
+  FastDiv div_s, div_w, div_p;
+  unsigned long long* work_counter;  // kQueues heads, kShardStride apart
+  unsigned long long* ray_counter;   // kQueues counter sets (as TraceArgs)
+  const DevMaterial* __restrict__ mats;
+  // per resident lane, the attenuating (non-dielectric) hits of its path:
+  // path[k * path_stride + lane slot], k < max_depth
+  int* __restrict__ path;
+  unsigned path_stride;
+};
+
+template <bool kBVH>
+__global__ void psrt_trace_mat(const double4* __restrict__ geo, const double* __restrict__ inv_r,
+                               double* __restrict__ rgb, MatArgs a, BvhView bv);
+// psrt_reduce over colour records: samp_t holds [pixels][s_count][3] doubles
+__global__ void psrt_reduce_rgb(ReduceArgs a);
+
 template <bool kBVH, bool kStamps, bool kLds, bool kCount>
 __global__ void psrt_trace(const double4* __restrict__ geo, const double* __restrict__ inv_r,
                            double* __restrict__ samples, TraceArgs a, BvhView bv);

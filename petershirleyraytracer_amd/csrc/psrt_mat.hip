@@ -1,0 +1,408 @@
+// psrt_mat.hip — the material integrator.
+//
+// A kernel variant of its own: the reference integrator (psrt_trace,
+// psrt_kernels.hip) keeps its code, bits and RNG consumption. This one traces
+// the book's continuation of the reference (Ray Tracing in One Weekend v3.2,
+// ch. 9-13; DESIGN.md §14 restates it):
+//
+//   psrt_trace_mat   persistent lanes, one camera sample per work unit:
+//                    thin-lens get_ray, then ray_color as a bounce loop —
+//                    world.hit(r, 0.001, inf) (hittable_list.cc:3-20 /
+//                    sphere.cc:3-40 over [tmin, closest]), lambertian / metal /
+//                    dielectric scatter; a finished sample stores its colour
+//                    (3 doubles) in unit order.
+//   psrt_reduce_rgb  pixel_color += sample in sample order (main.cc:77-84),
+//                    then write_color (color.h:8-24) on the last chunk.
+//
+// The recursion's product attenuation * ray_color(...) is taken innermost
+// first, so it is formed when the path ends: each lane keeps the indices of
+// the attenuating hits of its path in a scratch column (MatArgs::path;
+// dielectric hits attenuate by exactly 1 and are not kept), and multiplies
+// the sky colour by their albedos in reverse.
+//
+// Culling: the BVH (psrt_bvh.h) bounds every sphere with a root in
+// [0, closest], so it bounds [0.001, closest] too; each lane walks it on its
+// own (stackless skip links). Ties and the root rule are the reference's:
+// the lexicographic minimum of (t, -index), t = near root if >= tmin, else
+// far root if >= tmin. Rays the BVH cannot bound take the linear scan.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rt.h"
+#include "psrt_device.h"
+#include "psrt_geom.h"
+#include "psrt_kernels.h"
+
+namespace psrt {
+namespace {
+
+constexpr double kTmin = 0.001;  // the book's world.hit(r, 0.001, infinity)
+
+__device__ __forceinline__ unsigned div_fast(unsigned n, const FastDiv& f) {
+  const unsigned t = __umulhi(f.m, n);
+  return (t + ((n - t) >> f.sh1)) >> f.sh2;
+}
+
+__device__ __forceinline__ unsigned lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
+// random_double(-1, 1) (random.h:10-14): min + (max - min) * random_double()
+__device__ __forceinline__ double pm1(uint64_t& rng) { return -1.0 + 2.0 * random_double(rng); }
+
+// vec3::random_in_unit_sphere (vec3.h:83-95): draws z, y, x (g++ order)
+__device__ __forceinline__ void in_unit_sphere(uint64_t& rng, double& x, double& y, double& z) {
+  for (;;) {
+    z = pm1(rng);
+    y = pm1(rng);
+    x = pm1(rng);
+    if (!((x * x + y * y) + z * z > 1.0)) return;
+  }
+}
+
+// sphere.cc:6-31 over [tmin, bt], then the (t, index) rule. In ascending
+// index order from bt = inf this is the reference's scan exactly (NaN
+// included: a NaN root passes both range tests, as there).
+__device__ __forceinline__ void test_sphere_m(const double4 s, int idx, double ox, double oy,
+                                              double oz, double dx, double dy, double dz, double A,
+                                              double& bt, int& bi) {
+  const double ax = ox - s.x, ay = oy - s.y, az = oz - s.z;
+  const double hb = (dx * ax + dy * ay) + dz * az;
+  const double c = ((ax * ax + ay * ay) + az * az) - s.w;
+  const double disc = hb * hb - A * c;
+  if (disc < 0.0) return;
+  const double sq = sqrt_f64(disc);
+  double t = (-hb - sq) / A;
+  if (t < kTmin || t > bt) {
+    t = (-hb + sq) / A;
+    if (t < kTmin || t > bt) return;
+  }
+  if (t < bt || idx > bi) {  // equal t: the later index wins (sphere.cc:26 accepts t == tmax)
+    bt = t;
+    bi = idx;
+  }
+}
+
+// hittable_list::hit(r, 0.001, inf) for one lane.
+template <bool kBVH>
+__device__ __forceinline__ int world_hit_m(const double4* __restrict__ geo, int n,
+                                           const BvhView& bv, double ox, double oy, double oz,
+                                           double dx, double dy, double dz, double A, double& bt) {
+  bt = __builtin_inf();
+  int bi = -1;
+  const double am = __builtin_fmax(__builtin_fabs(ox),
+                                   __builtin_fmax(__builtin_fabs(oy), __builtin_fabs(oz)));
+  // unbounded arithmetic or no BVH: the reference scan, verbatim
+  if (!kBVH || !(A > 0.0 && A < 1e200) || !(am < 1e200)) {
+    for (int i = 0; i < n; ++i) test_sphere_m(geo[i], i, ox, oy, oz, dx, dy, dz, A, bt, bi);
+    return bi;
+  }
+  for (int b = 0; b < bv.n_big; ++b) {
+    const int idx = bv.big_idx[b];
+    test_sphere_m(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
+  }
+  // Far origins are re-based at their root-box entry (as hit_traverse): the
+  // FP32 slab test then sees coordinates of the scene's scale.
+  double t0 = 0.0;
+  if (!(am <= bv.r_check)) {
+    const double e = root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt);
+    if (e < 0.0) return bi;  // the segment [0, bt] misses every BVH sphere's padded box
+    t0 = e;
+  }
+  const float fox = (float)(ox + t0 * dx), foy = (float)(oy + t0 * dy), foz = (float)(oz + t0 * dz);
+  const float ix = safe_inv((float)dx), iy = safe_inv((float)dy), iz = safe_inv((float)dz);
+  const float oix = fox * ix, oiy = foy * iy, oiz = foz * iz;
+  const float tlo = -(float)t0 * 1.00000048f;
+  float tmax = tmax_up(bt - t0);
+  int node = 0;
+  while (node < bv.n_nodes) {
+    const float4 n0 = bv.nodes[2 * node], n1 = bv.nodes[2 * node + 1];
+    const int skip = __float_as_int(n1.z), leaf = __float_as_int(n1.w);
+    if (!slab_hit(n0, n1, ix, iy, iz, oix, oiy, oiz, tlo, tmax)) {
+      node = skip;
+    } else if (leaf < 0) {
+      ++node;  // interior hit: DFS order continues at node + 1
+    } else {
+      const int first = leaf >> 8, cnt = leaf & 255;
+      for (int k = first; k < first + cnt; ++k)
+        test_sphere_m(bv.leaf_geo[k], bv.leaf_idx[k], ox, oy, oz, dx, dy, dz, A, bt, bi);
+      tmax = tmax_up(bt - t0);
+      node = skip;
+    }
+  }
+  return bi;
+}
+
+// Schlick's approximation (book ch. 10.4), pow(x, 5) as (x*x)*(x*x)*x
+__device__ __forceinline__ double reflectance(double cosine, double ref) {
+  double r0 = (1.0 - ref) / (1.0 + ref);
+  r0 = r0 * r0;
+  const double x = 1.0 - cosine, x2 = x * x;
+  return r0 + (1.0 - r0) * ((x2 * x2) * x);
+}
+
+}  // namespace
+
+template <bool kBVH>
+__global__ __launch_bounds__(kMatBlock) void psrt_trace_mat(const double4* __restrict__ geo,
+                                                            const double* __restrict__ inv_r,
+                                                            double* __restrict__ rgb, MatArgs a,
+                                                            BvhView bv) {
+  const unsigned lane = __lane_id();
+  const uint64_t total = a.total_units;
+  int* const path = a.path + (size_t)blockIdx.x * kMatBlock + threadIdx.x;
+  const size_t ps = a.path_stride;
+
+  uint64_t win_base = 0;
+  unsigned win_left = 0;
+  unsigned qnext = 0;  // heads found past the end of the work (this block's first)
+  bool exhausted = false;
+
+  bool active = false;
+  double ox = 0, oy = 0, oz = 0, dx = 0, dy = 0, dz = 0, A = 0;
+  int k = 0, np = 0;  // hits so far / attenuating hits kept in `path`
+  uint64_t rng = 0;
+  unsigned su = 0;
+  unsigned long long rays = 0;
+
+  for (;;) {
+    // ---- refill idle lanes from the wave's window (ballot + mbcnt) ----
+    const uint64_t need = __ballot(!active);
+    if (need != 0 && !exhausted) {
+      const unsigned cnt = (unsigned)__popcll(need), rank = lanes_below(need);
+      uint64_t nb = 0;
+      bool fresh = false;
+      if (cnt > win_left) {
+        // sharded heads (psrt_kernels.h kQueues): global ticket g = t * kQueues + h
+        while (qnext < (unsigned)kQueues) {
+          const unsigned h = (blockIdx.x + qnext) % kQueues;
+          uint64_t tk = 0;
+          if (lane == 0) tk = atomicAdd(a.work_counter + kShardStride * h, 1ull);
+          tk = __shfl(tk, 0);
+          nb = (tk * kQueues + h) * kMatChunk;
+          if (nb < total) {
+            fresh = true;
+            break;
+          }
+          ++qnext;
+        }
+      }
+      if (!active) {
+        uint64_t unit = ~0ull;
+        if (rank < win_left) unit = win_base + rank;
+        else if (fresh) unit = nb + (rank - win_left);
+        if (unit < total) {
+          su = (unsigned)unit;
+          unsigned q = div_fast(su, a.div_s);  // f * pixels + pixel (frame-major units)
+          const unsigned sl = su - q * a.div_s.d;
+          unsigned f = 0;
+          if (a.frames > 1) {
+            f = div_fast(q, a.div_p);
+            q -= f * a.div_p.d;
+          }
+          const unsigned row_k = div_fast(q, a.div_w);
+          const unsigned i = q - row_k * a.div_w.d;
+          const int j = (a.height - 1) - (a.row_offset + (int)row_k * a.row_stride);
+          const unsigned pix = (unsigned)j * (unsigned)a.width + i;
+          const unsigned s = (unsigned)a.s_begin + sl;
+          rng = splitmix64((((uint64_t)pix) << 32 | (uint64_t)s) ^ a.seedmix[f]);
+          // main.cc:80-81
+          const double u = ((double)i + random_double(rng)) / (double)(a.width - 1);
+          const double v = ((double)j + random_double(rng)) / (double)(a.height - 1);
+          // thin lens (book ch. 12): rd = lens_radius * random_in_unit_disk()
+          // (vec3(random_double(-1,1), random_double(-1,1), 0): draws y, x)
+          double px, py;
+          for (;;) {
+            py = pm1(rng);
+            px = pm1(rng);
+            if (!((px * px + py * py) + 0.0 * 0.0 >= 1.0)) break;
+          }
+          const double rx = a.lens_radius * px, ry = a.lens_radius * py;
+          const double fx = a.lu[0] * rx + a.lv[0] * ry;
+          const double fy = a.lu[1] * rx + a.lv[1] * ry;
+          const double fz = a.lu[2] * rx + a.lv[2] * ry;
+          ox = a.org[0] + fx;
+          oy = a.org[1] + fy;
+          oz = a.org[2] + fz;
+          dx = (((a.llc[0] + u * a.hor[0]) + v * a.ver[0]) - a.org[0]) - fx;
+          dy = (((a.llc[1] + u * a.hor[1]) + v * a.ver[1]) - a.org[1]) - fy;
+          dz = (((a.llc[2] + u * a.hor[2]) + v * a.ver[2]) - a.org[2]) - fz;
+          A = (dx * dx + dy * dy) + dz * dz;
+          k = 0;
+          np = 0;
+          active = true;
+        }
+      }
+      if (cnt > win_left) {
+        if (fresh) {
+          win_base = nb + (cnt - win_left);
+          win_left = kMatChunk - (cnt - win_left);
+        } else {
+          win_left = 0;
+          exhausted = true;
+        }
+      } else {
+        win_base += cnt;
+        win_left -= cnt;
+      }
+    }
+    if (__ballot(active) == 0) break;
+    if (!active) continue;
+
+    // ---- one bounce of ray_color (book ch. 9-10) ----
+    bool fin = false;
+    double cr = 0.0, cg = 0.0, cb = 0.0;  // black: depth exhausted or absorbed
+    if (k >= a.max_depth) {
+      fin = true;  // depth <= 0
+    } else {
+      ++rays;
+      double bt;
+      const int bi = world_hit_m<kBVH>(geo, a.n, bv, ox, oy, oz, dx, dy, dz, A, bt);
+      if (bi < 0) {
+        // sky (main.cc:46-48), then attenuation * (...) innermost first
+        const double y = (1.0 / __builtin_sqrt(A)) * dy;
+        const double t = 0.5 * (y + 1.0);
+        cr = (1.0 - t) * 1.0 + t * 0.5;
+        cg = (1.0 - t) * 1.0 + t * 0.7;
+        cb = (1.0 - t) * 1.0 + t * 1.0;
+        for (int e = np - 1; e >= 0; --e) {
+          const DevMaterial& m = a.mats[path[(size_t)e * ps]];
+          cr = m.albedo[0] * cr;
+          cg = m.albedo[1] * cg;
+          cb = m.albedo[2] * cb;
+        }
+        fin = true;
+      } else {
+        const HitRec h = hit_record_of(geo[bi], inv_r[bi], bt, ox, oy, oz, dx, dy, dz);
+        const DevMaterial& m = a.mats[bi];
+        const int kind = m.kind;
+        double ndx, ndy, ndz;
+        bool ok = true;
+        if (kind == RT_MAT_LAMBERTIAN) {
+          // normal + random_unit_vector(); the normal if that is near zero
+          double x, y, z;
+          in_unit_sphere(rng, x, y, z);
+          const double inv = 1.0 / __builtin_sqrt((x * x + y * y) + z * z);
+          ndx = h.nx + inv * x;
+          ndy = h.ny + inv * y;
+          ndz = h.nz + inv * z;
+          if (__builtin_fabs(ndx) < 1e-8 && __builtin_fabs(ndy) < 1e-8 && __builtin_fabs(ndz) < 1e-8)
+            ndx = h.nx, ndy = h.ny, ndz = h.nz;
+        } else {
+          const double inv = 1.0 / __builtin_sqrt(A);
+          const double ux = inv * dx, uy = inv * dy, uz = inv * dz;
+          bool reflect = true;
+          double ratio = 0.0, ct = 0.0;
+          if (kind == RT_MAT_DIELECTRIC) {
+            ratio = h.front ? (1.0 / m.ir) : m.ir;
+            ct = __builtin_fmin(((-ux) * h.nx + (-uy) * h.ny) + (-uz) * h.nz, 1.0);
+            const double st = __builtin_sqrt(1.0 - ct * ct);
+            // cannot_refract || reflectance(...) > random_double()
+            reflect = ratio * st > 1.0 || reflectance(ct, ratio) > random_double(rng);
+          }
+          if (reflect) {  // reflect(v, n) = v - 2*dot(v,n)*n
+            const double dn = (ux * h.nx + uy * h.ny) + uz * h.nz;
+            ndx = ux - (2.0 * dn) * h.nx;
+            ndy = uy - (2.0 * dn) * h.ny;
+            ndz = uz - (2.0 * dn) * h.nz;
+          } else {  // refract(uv, n, ratio), cos_theta = ct
+            const double qx = ratio * (ux + ct * h.nx);
+            const double qy = ratio * (uy + ct * h.ny);
+            const double qz = ratio * (uz + ct * h.nz);
+            const double par = -__builtin_sqrt(__builtin_fabs(1.0 - ((qx * qx + qy * qy) + qz * qz)));
+            ndx = qx + par * h.nx;
+            ndy = qy + par * h.ny;
+            ndz = qz + par * h.nz;
+          }
+          if (kind == RT_MAT_METAL) {  // + fuzz * random_in_unit_sphere(); absorbed unless outward
+            double x, y, z;
+            in_unit_sphere(rng, x, y, z);
+            ndx = ndx + m.fuzz * x;
+            ndy = ndy + m.fuzz * y;
+            ndz = ndz + m.fuzz * z;
+            ok = ((ndx * h.nx + ndy * h.ny) + ndz * h.nz) > 0.0;
+          }
+        }
+        if (!ok) {
+          fin = true;
+        } else {
+          if (kind != RT_MAT_DIELECTRIC) path[(size_t)np++ * ps] = bi;
+          ox = h.px, oy = h.py, oz = h.pz;
+          dx = ndx, dy = ndy, dz = ndz;
+          A = (dx * dx + dy * dy) + dz * dz;
+          ++k;
+        }
+      }
+    }
+    if (fin) {
+      double* const o = rgb + 3 * (size_t)su;
+      o[0] = cr;
+      o[1] = cg;
+      o[2] = cb;
+      active = false;
+    }
+  }
+  // rays (== traced rays: no trapped-path shortcut here) -> this block's counter set
+  for (int off = 32; off > 0; off >>= 1) rays += __shfl_xor(rays, off);
+  if (lane == 0 && rays) {
+    unsigned long long* const ctr = a.ray_counter + kShardStride * (blockIdx.x % kQueues);
+    atomicAdd(ctr, rays);
+    atomicAdd(ctr + 3, rays);
+  }
+}
+
+template __global__ void psrt_trace_mat<false>(const double4* __restrict__,
+                                               const double* __restrict__, double* __restrict__,
+                                               MatArgs, BvhView);
+template __global__ void psrt_trace_mat<true>(const double4* __restrict__,
+                                              const double* __restrict__, double* __restrict__,
+                                              MatArgs, BvhView);
+
+// pixel_color += sample (main.cc:77-84) over colour records, in sample order;
+// write_color (color.h:8-24) on the last chunk. One lane per pixel; block 0
+// folds the trace launch's counter sets as psrt_reduce does.
+__global__ __launch_bounds__(kReduceBlock) void psrt_reduce_rgb(ReduceArgs a) {
+  if (blockIdx.x == 0 && a.fold_stats) {
+    if (threadIdx.x < 4) {
+      unsigned long long v = a.first_chunk ? 0ull : a.totals[threadIdx.x];
+      for (int h = 0; h < kQueues; ++h) {
+        v += a.sets[kShardStride * h + threadIdx.x];
+        a.sets[kShardStride * h + threadIdx.x] = 0ull;
+      }
+      a.totals[threadIdx.x] = v;
+      if (a.host_stats) a.host_stats[threadIdx.x] = v;
+    }
+    if (threadIdx.x < kQueues) a.heads[kShardStride * threadIdx.x] = 0ull;
+  }
+  const unsigned q = blockIdx.x * kReduceBlock + threadIdx.x;
+  if (q >= a.pixels) return;
+  double r = 0.0, g = 0.0, b = 0.0;
+  if (!a.first_chunk) {
+    r = a.accum[(size_t)q * 3 + 0];
+    g = a.accum[(size_t)q * 3 + 1];
+    b = a.accum[(size_t)q * 3 + 2];
+  }
+  const double* __restrict__ c = a.samp_t + (size_t)q * a.s_count * 3;
+  for (int s = 0; s < a.s_count; ++s) {
+    r += c[3 * s + 0];
+    g += c[3 * s + 1];
+    b += c[3 * s + 2];
+  }
+  if (a.accum) {
+    a.accum[(size_t)q * 3 + 0] = r;
+    a.accum[(size_t)q * 3 + 1] = g;
+    a.accum[(size_t)q * 3 + 2] = b;
+  }
+  if (a.rgb8) {
+    const double inv = 1.0 / (double)a.spp_total;
+    const double cc[3] = {r, g, b};
+    for (int ch = 0; ch < 3; ++ch) {
+      double x = __builtin_sqrt(cc[ch] * inv);
+      x = (x < 0.0) ? 0.0 : x;      // std::max(x, 0.0)
+      x = (0.999 < x) ? 0.999 : x;  // std::min(x, 0.999)
+      a.rgb8[(size_t)q * 3 + ch] = (unsigned char)(int)(255.999 * x);
+    }
+  }
+}
+
+}  // namespace psrt

@@ -98,6 +98,81 @@ int rt_camera_look_at(const double lookfrom[3], const double lookat[3], const do
   return RT_OK;
 }
 
+// The book's thin-lens camera (Ray Tracing in One Weekend v3.2, ch. 12), in
+// the reference's vec3 arithmetic: horizontal = (focus_dist * vw) * u, etc.
+int rt_camera_look_at_lens(const double lookfrom[3], const double lookat[3], const double vup[3],
+                           double vfov_deg, double aspect, double aperture, double focus_dist,
+                           rt_camera_lens* out) {
+  if (!lookfrom || !lookat || !vup || !out || !(aspect > 0) || !(aperture >= 0) ||
+      !(focus_dist > 0))
+    return RT_E_INVALID;
+  const double theta = vfov_deg * 3.1415926535897932385 / 180.0;  // raytracer.h:15-17
+  const double vh = 2.0 * std::tan(theta / 2);
+  const double vw = aspect * vh;
+  const d3 from{lookfrom[0], lookfrom[1], lookfrom[2]};
+  const d3 at{lookat[0], lookat[1], lookat[2]};
+  const d3 up{vup[0], vup[1], vup[2]};
+  const d3 w = unit(from - at);
+  const d3 u = unit(cross(up, w));
+  const d3 v = cross(w, u);
+  const d3 h = (focus_dist * vw) * u, vv = (focus_dist * vh) * v;
+  const d3 llc = ((from - over(h, 2.0)) - over(vv, 2.0)) - focus_dist * w;
+  put(&out->base, from, llc, h, vv);
+  out->u[0] = u.x, out->u[1] = u.y, out->u[2] = u.z;
+  out->v[0] = v.x, out->v[1] = v.y, out->v[2] = v.z;
+  out->lens_radius = aperture / 2;
+  return RT_OK;
+}
+
+// The book's random_scene() (ch. 13) with materials, on the glibc srand(seed)
+// stream. Every vec3 built from draws takes them in g++'s order (constructor
+// arguments right to left: z, then y, then x), and color::random() *
+// color::random() evaluates its right operand first.
+int rt_scene_book_final(unsigned int seed, rt_sphere* out, rt_material* mats, int cap) {
+  GlibcStream g(seed);
+  int n = 0;
+  auto push = [&](double x, double y, double z, double r, rt_material m) {
+    if (out && n < cap) out[n] = rt_sphere{x, y, z, r};
+    if (mats && n < cap) mats[n] = m;
+    ++n;
+  };
+  auto lam = [](double r, double gg, double b) {
+    return rt_material{RT_MAT_LAMBERTIAN, 0, {r, gg, b}, 0.0, 0.0};
+  };
+  auto rnd3 = [&](double lo, double hi, double c[3]) {  // vec3::random(lo, hi): z, y, x
+    c[2] = lo + (hi - lo) * g.uniform();
+    c[1] = lo + (hi - lo) * g.uniform();
+    c[0] = lo + (hi - lo) * g.uniform();
+  };
+  push(0.0, -1000.0, 0.0, 1000.0, lam(0.5, 0.5, 0.5));
+  for (int a = -11; a < 11; ++a) {
+    for (int b = -11; b < 11; ++b) {
+      const double choose = g.uniform();
+      const double cz = b + 0.9 * g.uniform();  // point3(a + 0.9 rd, 0.2, b + 0.9 rd): z first
+      const double cx = a + 0.9 * g.uniform();
+      const d3 c{cx, 0.2, cz};
+      if (!(len(c - d3{4, 0.2, 0}) > 0.9)) continue;
+      if (choose < 0.8) {  // diffuse: albedo = color::random() * color::random()
+        double rb[3], ra[3];
+        rnd3(0.0, 1.0, rb);  // the right operand is evaluated first
+        rnd3(0.0, 1.0, ra);
+        push(cx, 0.2, cz, 0.2, lam(ra[0] * rb[0], ra[1] * rb[1], ra[2] * rb[2]));
+      } else if (choose < 0.95) {  // metal
+        double al[3];
+        rnd3(0.5, 1.0, al);
+        const double fuzz = 0.0 + (0.5 - 0.0) * g.uniform();
+        push(cx, 0.2, cz, 0.2, rt_material{RT_MAT_METAL, 0, {al[0], al[1], al[2]}, fuzz, 0.0});
+      } else {  // glass
+        push(cx, 0.2, cz, 0.2, rt_material{RT_MAT_DIELECTRIC, 0, {1.0, 1.0, 1.0}, 0.0, 1.5});
+      }
+    }
+  }
+  push(0.0, 1.0, 0.0, 1.0, rt_material{RT_MAT_DIELECTRIC, 0, {1.0, 1.0, 1.0}, 0.0, 1.5});
+  push(-4.0, 1.0, 0.0, 1.0, lam(0.4, 0.2, 0.1));
+  push(4.0, 1.0, 0.0, 1.0, rt_material{RT_MAT_METAL, 0, {0.7, 0.6, 0.5}, 0.0, 0.0});
+  return n;
+}
+
 int rt_scene_two_spheres(rt_sphere* out, int cap) {
   // main.cc:62-63
   const rt_sphere s[2] = {{0.0, 0.0, -1.0, 0.5}, {0.0, -100.5, 0.0, 100.0}};

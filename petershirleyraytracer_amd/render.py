@@ -9,6 +9,8 @@ Mirrors the reference's pieces by name and meaning:
 * ``load_scene / parse_scene``    scene/camera files (DESIGN.md §Scene files)
 * ``save_scene / format_scene``   ... and back (bit-exact round trip)
 * ``render(...)``                 the main.cc:72-88 pixel loop for a shard of rows
+* ``render_materials(...)``       the book's material integrator + thin lens
+                                  (extension; parity unpinned)
 * ``write_ppm(...)``              main.cc:70 header + color.h:21-23 pixel lines
 
 Scenes are ``(n, 4)`` float64 arrays of (cx, cy, cz, r) in hittable_list order;
@@ -23,7 +25,7 @@ from typing import Optional
 import numpy as np
 
 from . import _lib
-from ._lib import RtCamera, RtParams, RtSphere, RtStats, check
+from ._lib import RtCamera, RtCameraLens, RtMaterial, RtParams, RtSphere, RtStats, check
 
 
 def _spheres(spheres) -> tuple:
@@ -52,6 +54,68 @@ FLAG_NO_CULL = 1
 FLAG_NO_FIXPOINT = 2  # trace provably trapped paths to max_depth (same bits, slower)
 FLAG_NO_TAIL_PRIORITY = 4  # scheduling hint: no issue priority for the launch tail (same bits)
 FLAG_CULL_STATS = 8  # count executed sphere / box tests (slower kernel variant; else they read 0)
+FLAG_MATERIALS = 16  # the material integrator of the context (rt_context_set_materials)
+
+# Materials are (n, 6) float64 rows (kind, albedo r, g, b, fuzz, ir), one per
+# sphere in hittable_list order (include/rt.h rt_material).
+MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC = 0, 1, 2
+
+
+def _materials(mats) -> tuple:
+    a = np.asarray(mats, dtype=np.float64).reshape(-1, 6)
+    buf = (RtMaterial * max(1, len(a)))()
+    for k, row in enumerate(a):
+        buf[k].kind = int(row[0])
+        buf[k].albedo[0], buf[k].albedo[1], buf[k].albedo[2] = row[1], row[2], row[3]
+        buf[k].fuzz, buf[k].ir = row[4], row[5]
+    return buf, len(a)
+
+
+def _materials_array(buf, n: int) -> np.ndarray:
+    return np.array([[buf[k].kind, *list(buf[k].albedo), buf[k].fuzz, buf[k].ir]
+                     for k in range(n)], dtype=np.float64).reshape(n, 6)
+
+
+@dataclass
+class LensCamera:
+    """The book's thin-lens camera (rt_camera_lens): the focus-plane basis
+    (4, 3) as camera arrays, the lens axes u, v and lens_radius."""
+    base: np.ndarray
+    u: np.ndarray
+    v: np.ndarray
+    lens_radius: float
+
+    def to_c(self) -> RtCameraLens:
+        c = RtCameraLens()
+        c.base = _camera(self.base)
+        for k in range(3):
+            c.u[k], c.v[k] = float(self.u[k]), float(self.v[k])
+        c.lens_radius = float(self.lens_radius)
+        return c
+
+
+def camera_look_at_lens(lookfrom=(13.0, 2.0, 3.0), lookat=(0.0, 0.0, 0.0), vup=(0.0, 1.0, 0.0),
+                        vfov: float = 20.0, aspect: float = 1.5, aperture: float = 0.1,
+                        focus_dist: float = 10.0) -> LensCamera:
+    """camera(lookfrom, lookat, vup, vfov, aspect, aperture, focus_dist) (book ch. 12)."""
+    c = RtCameraLens()
+    d3 = C.c_double * 3
+    check(_lib.load().rt_camera_look_at_lens(d3(*lookfrom), d3(*lookat), d3(*vup), vfov, aspect,
+                                             aperture, focus_dist, C.byref(c)),
+          "rt_camera_look_at_lens")
+    return LensCamera(_camera_array(c.base), np.array(list(c.u)), np.array(list(c.v)),
+                      c.lens_radius)
+
+
+def scene_book_final(seed: int = 1):
+    """The book's random_scene() with materials: (spheres (n, 4), materials (n, 6))."""
+    L = _lib.load()
+    n = L.rt_scene_book_final(seed, None, None, 0)
+    sp = (RtSphere * n)()
+    mt = (RtMaterial * n)()
+    L.rt_scene_book_final(seed, sp, mt, n)
+    return (np.frombuffer(sp, dtype=np.float64, count=4 * n).reshape(n, 4).copy(),
+            _materials_array(mt, n))
 
 
 def params(width: int, height: int, spp: int, max_depth: int = 50, seed: int = 0,
@@ -183,6 +247,30 @@ def render(spheres, camera, width: int, height: int, spp: int, max_depth: int = 
     return acc, rgb, stats_dict(st)
 
 
+def render_materials(spheres, materials, camera: LensCamera, width: int, height: int, spp: int,
+                     max_depth: int = 50, seed: int = 0, row_offset: int = 0, row_stride: int = 1,
+                     want_rgb: bool = True, cull: bool = True):
+    """One-shot render with the material integrator (rt_render_materials).
+    Returns (accum[rows, W, 3] float64, rgb8 or None, stats dict)."""
+    L = _lib.load()
+    sp, n = _spheres(spheres)
+    mt, nm = _materials(materials)
+    if nm != n:
+        raise ValueError("one material per sphere")
+    cam = camera.to_c()
+    p = params(width, height, spp, max_depth, seed, row_offset, row_stride,
+               FLAG_MATERIALS | (0 if cull else FLAG_NO_CULL))
+    rows = max(0, L.rt_rows_owned(height, row_offset, row_stride))
+    acc = np.zeros((rows, width, 3), dtype=np.float64)
+    rgb = np.zeros((rows, width, 3), dtype=np.uint8) if want_rgb else None
+    st = RtStats()
+    check(L.rt_render_materials(sp, mt, n, C.byref(cam), C.byref(p),
+                                acc.ctypes.data_as(C.POINTER(C.c_double)),
+                                rgb.ctypes.data_as(C.POINTER(C.c_ubyte)) if rgb is not None
+                                else None, C.byref(st)), "rt_render_materials")
+    return acc, rgb, stats_dict(st)
+
+
 def quantize(accum: np.ndarray, spp: int) -> np.ndarray:
     """write_color (color.h:8-24) on host accumulators."""
     acc = np.ascontiguousarray(accum, dtype=np.float64)
@@ -209,6 +297,18 @@ class Context:
         cam = _camera(camera)
         check(self._L.rt_context_set_scene(self.handle, sp, n, C.byref(cam)),
               "rt_context_set_scene")
+
+    def set_materials(self, materials, camera: Optional[LensCamera]) -> None:
+        """Materials (n, 6) for the scene's spheres and the lens camera of
+        renders with FLAG_MATERIALS; materials=None clears them."""
+        if materials is None:
+            check(self._L.rt_context_set_materials(self.handle, None, 0, None),
+                  "rt_context_set_materials")
+            return
+        mt, n = _materials(materials)
+        cam = camera.to_c()
+        check(self._L.rt_context_set_materials(self.handle, mt, n, C.byref(cam)),
+              "rt_context_set_materials")
 
     def render_device(self, p: RtParams, d_accum: int = 0, d_rgb8: int = 0,
                       stream: int = 0) -> None:

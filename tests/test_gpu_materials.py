@@ -1,0 +1,109 @@
+"""Materials and defocus on the device (psrt_trace_mat).
+
+Bit-exact against oracle/rt_oracle_mat.c (pinned to tests/mat_pyref.py by
+test_materials.py). Parity with the reference itself is unpinned: the
+reference has no materials.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import bits
+
+import petershirleyraytracer_amd as P
+from petershirleyraytracer_amd import _lib
+from petershirleyraytracer_amd.render import FLAG_MATERIALS, FLAG_NO_CULL, LensCamera
+from test_materials import MIXED_MATS, MIXED_SPHERES, mixed_lens
+
+pytestmark = pytest.mark.gpu
+
+
+def _lens(d) -> LensCamera:
+    return LensCamera(d["base"], d["u"], d["v"], d["lens_radius"])
+
+
+@pytest.fixture(scope="module")
+def book(oracle_mod):
+    sp, mt = oracle_mod.scene_book_final(1)
+    return sp, mt, oracle_mod.camera_look_at_lens(aspect=1.5)
+
+
+@pytest.mark.parametrize("cull", [True, False])
+def test_book_scene_bit_exact(oracle_mod, book, cull):
+    sp, mt, lens = book
+    W, H, spp, seed = 72, 48, 4, 9
+    acc, rgb, st = P.render_materials(sp, mt, _lens(lens), W, H, spp, 50, seed, cull=cull)
+    ref, rays = oracle_mod.render_mat(sp, mt, lens, W, H, spp, 50, seed, threads=8)
+    assert np.array_equal(bits(acc), bits(ref))
+    assert np.array_equal(rgb, oracle_mod.quantize(ref, spp))
+    assert st["rays"] == rays and st["samples"] == W * H * spp
+
+
+def test_mixed_scene_bit_exact(oracle_mod):
+    lens = mixed_lens(oracle_mod)
+    W, H, spp, seed = 60, 40, 6, 2
+    acc, rgb, st = P.render_materials(MIXED_SPHERES, MIXED_MATS, _lens(lens), W, H, spp, 30, seed)
+    ref, rays = oracle_mod.render_mat(MIXED_SPHERES, MIXED_MATS, lens, W, H, spp, 30, seed,
+                                      threads=8)
+    assert np.array_equal(bits(acc), bits(ref))
+    assert st["rays"] == rays
+
+
+def test_shards_and_depth_edges(oracle_mod, book):
+    sp, mt, lens = book
+    W, H, spp = 40, 27, 2
+    full, _ = oracle_mod.render_mat(sp, mt, lens, W, H, spp, 8, 4, threads=8)
+    for off in range(3):
+        acc, _, _ = P.render_materials(sp, mt, _lens(lens), W, H, spp, 8, 4, off, 3)
+        assert np.array_equal(bits(acc), bits(full[off::3]))
+    for d in (0, -1):
+        acc, rgb, st = P.render_materials(sp, mt, _lens(lens), W, H, spp, d, 4)
+        assert not acc.any() and not rgb.any() and st["rays"] == 0
+    with pytest.raises(_lib.RtError):
+        P.render_materials(sp, mt, _lens(lens), W, H, spp, 4097, 4)
+
+
+def test_chunked_multi_frame_context(oracle_mod, book, monkeypatch):
+    """Sample chunks (a small buffer cap) and multi-frame launches through the
+    context: frame f equals the one-shot render of seed + f."""
+    import torch
+    sp, mt, lens = book
+    W, H, spp, seed, nf = 32, 20, 48, 21, 3
+    # 1 MiB holds 22 samples of 3 frames x 640 pixels x 24 B: 3 chunks of 16
+    monkeypatch.setenv("PSRT_SAMPLE_BUF_MB", "1")
+    ctx = P.Context(0)
+    try:
+        ctx.set_scene(sp, lens["base"])
+        with pytest.raises(_lib.RtError):  # no materials yet
+            ctx.render_device(P.params(W, H, spp, 50, seed, flags=FLAG_MATERIALS))
+        ctx.set_materials(mt, _lens(lens))
+        acc = [torch.zeros((H, W, 3), dtype=torch.float64, device="cuda") for _ in range(nf)]
+        rgb = [torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(nf)]
+        ctx.render_device_frames(P.params(W, H, spp, 50, seed, flags=FLAG_MATERIALS), nf,
+                                 [a.data_ptr() for a in acc], [r.data_ptr() for r in rgb])
+        st = ctx.sync_stats()
+        total = 0
+        for f in range(nf):
+            ref, rays = oracle_mod.render_mat(sp, mt, lens, W, H, spp, 50, seed + f, threads=8)
+            assert np.array_equal(bits(acc[f].cpu().numpy()), bits(ref)), f
+            assert np.array_equal(rgb[f].cpu().numpy(), oracle_mod.quantize(ref, spp)), f
+            total += rays
+        assert st["rays"] == total
+        # the same context, back to the reference integrator: unchanged bits
+        ctx.render_device(P.params(W, H, spp, 50, seed), acc[0].data_ptr())
+        ctx.sync_stats()
+        ref, _, _ = oracle_mod.render(sp, lens["base"], W, H, spp, 50, seed, threads=8)
+        assert np.array_equal(bits(acc[0].cpu().numpy()), bits(ref))
+    finally:
+        ctx.close()
+
+
+def test_lens_radius_zero_and_no_cull_flag(oracle_mod):
+    lens = mixed_lens(oracle_mod, aperture=0.0)
+    W, H, spp = 30, 20, 3
+    a, _, _ = P.render_materials(MIXED_SPHERES, MIXED_MATS, _lens(lens), W, H, spp, 50, 1,
+                                 cull=False)
+    ref, _ = oracle_mod.render_mat(MIXED_SPHERES, MIXED_MATS, lens, W, H, spp, 50, 1, threads=8)
+    assert np.array_equal(bits(a), bits(ref))
+    assert FLAG_NO_CULL == 1
