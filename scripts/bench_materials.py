@@ -1,0 +1,93 @@
+"""Throughput of the materials extension: the book's final scene
+(rt_scene_book_final, lens camera: aperture 0.1, focus 10, vfov 20, 3:2) at
+W x H x spp, max depth 50, on one GPU, with the C restatement timed on the
+host cores beside it (a bounded sample of rows).
+
+    python scripts/bench_materials.py [--width 1200 --height 800 --spp 10 --steps 3]
+
+Prints one JSON line. Frames are device-resident (no D2H in the timed region).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--width", type=int, default=1200)
+    ap.add_argument("--height", type=int, default=800)
+    ap.add_argument("--spp", type=int, default=10)
+    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--cpu-rows", type=int, default=8)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cull", action="store_true")
+    a = ap.parse_args()
+
+    import torch
+    import petershirleyraytracer_amd as P
+    from petershirleyraytracer_amd.render import FLAG_MATERIALS, FLAG_NO_CULL
+
+    W, H, S = a.width, a.height, a.spp
+    sp, mt = P.scene_book_final(1)
+    lens = P.camera_look_at_lens(aspect=W / H)
+    ctx = P.Context(0)
+    ctx.set_scene(sp, lens.base)
+    ctx.set_materials(mt, lens)
+    acc = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
+    rgb = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+    flags = FLAG_MATERIALS | (FLAG_NO_CULL if a.no_cull else 0)
+    st = ctx.stream()
+    for i in range(a.warmup):
+        ctx.render_device(P.params(W, H, S, a.depth, 100 + i, flags=flags), acc.data_ptr(),
+                          rgb.data_ptr(), st)
+        ctx.sync_stats()
+    ms, kms, rays = [], [], 0
+    for i in range(a.steps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ctx.render_device(P.params(W, H, S, a.depth, i, flags=flags), acc.data_ptr(),
+                          rgb.data_ptr(), st)
+        s = ctx.sync_stats()
+        ms.append((time.perf_counter() - t0) * 1e3)
+        kms.append(s["kernel_ms"])
+        rays += s["rays"]
+    step = sum(ms) / len(ms)
+    out = {
+        "metric": "Msamples/sec (materials extension, book final scene)",
+        "value": W * H * S / (step * 1e3),
+        "unit": "Msamples/s",
+        "ms_per_step": step,
+        "kernel_ms": sum(kms) / len(kms),
+        "grays_per_s": rays / (sum(ms) * 1e6),
+        "rays_per_sample": rays / (a.steps * W * H * S),
+        "config": {"scene": "book_final(seed 1), 487 spheres, lambertian/metal/dielectric",
+                   "width": W, "height": H, "spp": S, "max_depth": a.depth,
+                   "lens": "aperture 0.1, focus 10", "cull": not a.no_cull},
+        "steps": a.steps, "warmup": a.warmup, "dtype": "f64",
+    }
+    ctx.close()
+    # the C restatement on the host cores, a bounded sample of rows
+    import oracle
+    threads = a.cpu_threads or len(os.sched_getaffinity(0))
+    ol = oracle.camera_look_at_lens(aspect=W / H)
+    osp, omt = oracle.scene_book_final(1)
+    rows = a.cpu_rows
+    t0 = time.perf_counter()
+    _, crays = oracle.render_mat(osp, omt, ol, W, H, S, a.depth, 0, 0, max(1, H // rows),
+                                 threads=threads)
+    dt = time.perf_counter() - t0
+    n = oracle.rows_owned(H, 0, max(1, H // rows)) * W * S
+    out["cpu_baseline"] = {"value": n / (dt * 1e6), "unit": "Msamples/s", "cores": threads,
+                           "kind": "port", "sample": f"{n} samples ({n // (W * S)} rows)"}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
