@@ -281,10 +281,10 @@ int rt_context_create(int device, rt_context** out) {
       break;
     }
   }
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace_mat<false>,
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace_mat<false, false>,
                                                         psrt::kMatBlock, 0));
   c->grid_mat = c->cus * (per_cu < 1 ? 1 : per_cu);
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace_mat<true>,
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace_mat<true, false>,
                                                         psrt::kMatBlock, 0));
   c->grid_mat_bvh = c->cus * (per_cu < 1 ? 1 : per_cu);
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -665,8 +665,23 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
   if (rc) return rc;
   const bool use_bvh = c->bvh && !(p->flags & RT_FLAG_NO_CULL);
   psrt::MatArgs ma{};
+  // material kernel: the BVH staged in LDS when the workgroups resident per CU
+  // stay as many as without (PSRT_MAT_LDS=0/1 forces it off / on)
+  int mat_grid = use_bvh ? c->grid_mat_bvh : c->grid_mat;
+  unsigned mat_lds = 0;
+  if (mat && use_bvh) {
+    const unsigned bytes = psrt::mat_lds_bytes(c->n_nodes, c->n_leaf);
+    int pc = 0;
+    const char* ml = std::getenv("PSRT_MAT_LDS");
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, psrt::psrt_trace_mat<true, true>,
+                                                     psrt::kMatBlock, bytes) == hipSuccess &&
+        pc >= 1 && (ml ? std::atoi(ml) != 0 : c->cus * pc >= c->grid_mat_bvh)) {
+      mat_lds = bytes;
+      mat_grid = c->cus * pc;
+    }
+  }
   if (mat) {  // the path scratch: one column per resident lane, max_depth rows
-    const size_t lanes = (size_t)(use_bvh ? c->grid_mat_bvh : c->grid_mat) * psrt::kMatBlock;
+    const size_t lanes = (size_t)mat_grid * psrt::kMatBlock;
     const size_t need_ints = lanes * (size_t)std::max(1, p->max_depth);
     if (c->path_cap < need_ints) {
       rc = quiesce(c);
@@ -853,13 +868,18 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
       ma.div_s = ta.div_s;
       ma.total_units = ta.total_units;
       HIP_TRY(hipEventRecord(c->ev[2 * ch], st));
-      const int grid = use_bvh ? c->grid_mat_bvh : c->grid_mat;
-      if (use_bvh)
-        hipLaunchKernelGGL(psrt::psrt_trace_mat<true>, dim3(grid), dim3(psrt::kMatBlock), 0, st,
-                           c->d_geo, c->d_inv_r, c->d_samples, ma, bv);
+      if (mat_lds)
+        hipLaunchKernelGGL((psrt::psrt_trace_mat<true, true>), dim3(mat_grid),
+                           dim3(psrt::kMatBlock), mat_lds, st, c->d_geo, c->d_inv_r, c->d_samples,
+                           ma, bv);
+      else if (use_bvh)
+        hipLaunchKernelGGL((psrt::psrt_trace_mat<true, false>), dim3(mat_grid),
+                           dim3(psrt::kMatBlock), 0, st, c->d_geo, c->d_inv_r, c->d_samples, ma,
+                           bv);
       else
-        hipLaunchKernelGGL(psrt::psrt_trace_mat<false>, dim3(grid), dim3(psrt::kMatBlock), 0, st,
-                           c->d_geo, c->d_inv_r, c->d_samples, ma, bv);
+        hipLaunchKernelGGL((psrt::psrt_trace_mat<false, false>), dim3(mat_grid),
+                           dim3(psrt::kMatBlock), 0, st, c->d_geo, c->d_inv_r, c->d_samples, ma,
+                           bv);
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipEventRecord(c->ev[2 * ch + 1], st));
       for (size_t f = 0; f < nf; ++f) {

@@ -180,7 +180,14 @@ struct DevMaterial {
   int pad_;
 };
 static_assert(sizeof(DevMaterial) == 48, "device material layout");
-constexpr int kMatBlock = 256;
+#ifndef PSRT_MAT_BLOCK
+#define PSRT_MAT_BLOCK 320  // 5 waves: four workgroups (20 waves) per CU share 160 KB of LDS
+#endif
+constexpr int kMatBlock = PSRT_MAT_BLOCK;
+#ifndef PSRT_MAT_WAVES
+#define PSRT_MAT_WAVES 5  // waves per SIMD asked of the register allocator (96 VGPRs)
+#endif
+constexpr int kMatWaves = PSRT_MAT_WAVES;
 constexpr unsigned kMatChunk = 256;  // units per queue ticket
 constexpr int kMatMaxDepth = 4096;   // path scratch rows (max_depth bound of RT_FLAG_MATERIALS)
 // Sample record of the material path: the sample's colour, 3 doubles, in unit
@@ -207,7 +214,14 @@ struct MatArgs {
   unsigned path_stride;
 };
 
-template <bool kBVH>
+// psrt_trace_mat<true, true> stages the BVH in dynamic LDS: nodes (2 float4
+// each, plus the padding node), leaf spheres, leaf indices; byte size:
+__host__ __device__ inline unsigned mat_lds_bytes(int n_nodes, int n_leaf) {
+  return 32u * (unsigned)(n_nodes + 1) + 32u * (unsigned)n_leaf +
+         ((4u * (unsigned)n_leaf + 15u) & ~15u);
+}
+
+template <bool kBVH, bool kLds>
 __global__ void psrt_trace_mat(const double4* __restrict__ geo, const double* __restrict__ inv_r,
                                double* __restrict__ rgb, MatArgs a, BvhView bv);
 // psrt_reduce over colour records: samp_t holds [pixels][s_count][3] doubles

@@ -36,7 +36,8 @@
 namespace psrt {
 namespace {
 
-constexpr double kTmin = 0.001;  // the book's world.hit(r, 0.001, infinity)
+constexpr double kTmin = 0.001;
+  // the book's world.hit(r, 0.001, infinity)
 
 __device__ __forceinline__ unsigned div_fast(unsigned n, const FastDiv& f) {
   const unsigned t = __umulhi(f.m, n);
@@ -49,16 +50,6 @@ __device__ __forceinline__ unsigned lanes_below(uint64_t m) {
 
 // random_double(-1, 1) (random.h:10-14): min + (max - min) * random_double()
 __device__ __forceinline__ double pm1(uint64_t& rng) { return -1.0 + 2.0 * random_double(rng); }
-
-// vec3::random_in_unit_sphere (vec3.h:83-95): draws z, y, x (g++ order)
-__device__ __forceinline__ void in_unit_sphere(uint64_t& rng, double& x, double& y, double& z) {
-  for (;;) {
-    z = pm1(rng);
-    y = pm1(rng);
-    x = pm1(rng);
-    if (!((x * x + y * y) + z * z > 1.0)) return;
-  }
-}
 
 // sphere.cc:6-31 over [tmin, bt], then the (t, index) rule. In ascending
 // index order from bt = inf this is the reference's scan exactly (NaN
@@ -86,7 +77,9 @@ __device__ __forceinline__ void test_sphere_m(const double4 s, int idx, double o
 // hittable_list::hit(r, 0.001, inf) for one lane.
 template <bool kBVH>
 __device__ __forceinline__ int world_hit_m(const double4* __restrict__ geo, int n,
-                                           const BvhView& bv, double ox, double oy, double oz,
+                                           const BvhView& bv, const float4* __restrict__ nodes,
+                                           const double4* __restrict__ leaf_geo,
+                                           const int* __restrict__ leaf_idx, double ox, double oy, double oz,
                                            double dx, double dy, double dz, double A, double& bt) {
   bt = __builtin_inf();
   int bi = -1;
@@ -114,21 +107,29 @@ __device__ __forceinline__ int world_hit_m(const double4* __restrict__ geo, int 
   const float oix = fox * ix, oiy = foy * iy, oiz = foz * iz;
   const float tlo = -(float)t0 * 1.00000048f;
   float tmax = tmax_up(bt - t0);
+  // While-while (Aila & Laine 2009): a lane that reaches a leaf holds it
+  // until every lane of the wave holds one or is done; the held leaves' FP64
+  // tests then run together instead of once per trip in which any lane has one.
   int node = 0;
-  while (node < bv.n_nodes) {
-    const float4 n0 = bv.nodes[2 * node], n1 = bv.nodes[2 * node + 1];
-    const int skip = __float_as_int(n1.z), leaf = __float_as_int(n1.w);
-    if (!slab_hit(n0, n1, ix, iy, iz, oix, oiy, oiz, tlo, tmax)) {
-      node = skip;
-    } else if (leaf < 0) {
-      ++node;  // interior hit: DFS order continues at node + 1
-    } else {
-      const int first = leaf >> 8, cnt = leaf & 255;
-      for (int k = first; k < first + cnt; ++k)
-        test_sphere_m(bv.leaf_geo[k], bv.leaf_idx[k], ox, oy, oz, dx, dy, dz, A, bt, bi);
-      tmax = tmax_up(bt - t0);
-      node = skip;
+  for (;;) {
+    int leaf = -1;
+    while (node < bv.n_nodes && leaf < 0) {
+      const float4 n0 = nodes[2 * node], n1 = nodes[2 * node + 1];
+      const int skip = __float_as_int(n1.z), lf = __float_as_int(n1.w);
+      if (!slab_hit(n0, n1, ix, iy, iz, oix, oiy, oiz, tlo, tmax)) {
+        node = skip;
+      } else if (lf < 0) {
+        ++node;  // interior hit: DFS order continues at node + 1
+      } else {
+        leaf = lf;
+        node = skip;
+      }
     }
+    if (leaf < 0) break;
+    const int first = leaf >> 8, cnt = leaf & 255;
+    for (int k = first; k < first + cnt; ++k)
+      test_sphere_m(leaf_geo[k], leaf_idx[k], ox, oy, oz, dx, dy, dz, A, bt, bi);
+    tmax = tmax_up(bt - t0);
   }
   return bi;
 }
@@ -143,8 +144,8 @@ __device__ __forceinline__ double reflectance(double cosine, double ref) {
 
 }  // namespace
 
-template <bool kBVH>
-__global__ __launch_bounds__(kMatBlock) void psrt_trace_mat(const double4* __restrict__ geo,
+template <bool kBVH, bool kLds>
+__global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const double4* __restrict__ geo,
                                                             const double* __restrict__ inv_r,
                                                             double* __restrict__ rgb, MatArgs a,
                                                             BvhView bv) {
@@ -152,6 +153,23 @@ __global__ __launch_bounds__(kMatBlock) void psrt_trace_mat(const double4* __res
   const uint64_t total = a.total_units;
   int* const path = a.path + (size_t)blockIdx.x * kMatBlock + threadIdx.x;
   const size_t ps = a.path_stride;
+  // kLds: the BVH in dynamic LDS (mat_lds_bytes), so the walk's dependent
+  // node loads see LDS latency instead of L1 / L2 latency
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+  const float4* __restrict__ nodes = bv.nodes;
+  const double4* __restrict__ leaf_geo = bv.leaf_geo;
+  const int* __restrict__ leaf_idx = bv.leaf_idx;
+  if constexpr (kLds) {
+    float4* const sn = (float4*)s_dyn;
+    double4* const sg = (double4*)(s_dyn + 32u * (unsigned)(bv.n_nodes + 1));
+    int* const si = (int*)(s_dyn + 32u * (unsigned)(bv.n_nodes + 1) + 32u * (unsigned)bv.n_leaf);
+    for (int e = threadIdx.x; e < 2 * (bv.n_nodes + 1); e += kMatBlock) sn[e] = bv.nodes[e];
+    for (int e = threadIdx.x; e < bv.n_leaf; e += kMatBlock) sg[e] = bv.leaf_geo[e], si[e] = bv.leaf_idx[e];
+    __syncthreads();
+    nodes = sn;
+    leaf_geo = sg;
+    leaf_idx = si;
+  }
 
   uint64_t win_base = 0;
   unsigned win_left = 0;
@@ -161,7 +179,7 @@ __global__ __launch_bounds__(kMatBlock) void psrt_trace_mat(const double4* __res
   bool active = false;
   double ox = 0, oy = 0, oz = 0, dx = 0, dy = 0, dz = 0, A = 0;
   int k = 0, np = 0;  // hits so far / attenuating hits kept in `path`
-  uint64_t rng = 0;
+  uint64_t rng = 0;   // the sample's stream: position of its next draw
   unsigned su = 0;
   unsigned long long rays = 0;
 
@@ -247,91 +265,113 @@ __global__ __launch_bounds__(kMatBlock) void psrt_trace_mat(const double4* __res
       }
     }
     if (__ballot(active) == 0) break;
-    if (!active) continue;
 
-    // ---- one bounce of ray_color (book ch. 9-10) ----
-    bool fin = false;
+    // ---- world.hit(r, 0.001, inf) of this bounce (book ch. 9-10) ----
+    bool fin = false, resolved = false;
+    int pbi = -1;
+    double pbt = 0.0;
     double cr = 0.0, cg = 0.0, cb = 0.0;  // black: depth exhausted or absorbed
-    if (k >= a.max_depth) {
-      fin = true;  // depth <= 0
-    } else {
-      ++rays;
-      double bt;
-      const int bi = world_hit_m<kBVH>(geo, a.n, bv, ox, oy, oz, dx, dy, dz, A, bt);
-      if (bi < 0) {
-        // sky (main.cc:46-48), then attenuation * (...) innermost first
-        const double y = (1.0 / __builtin_sqrt(A)) * dy;
-        const double t = 0.5 * (y + 1.0);
-        cr = (1.0 - t) * 1.0 + t * 0.5;
-        cg = (1.0 - t) * 1.0 + t * 0.7;
-        cb = (1.0 - t) * 1.0 + t * 1.0;
-        for (int e = np - 1; e >= 0; --e) {
-          const DevMaterial& m = a.mats[path[(size_t)e * ps]];
-          cr = m.albedo[0] * cr;
-          cg = m.albedo[1] * cg;
-          cb = m.albedo[2] * cb;
-        }
-        fin = true;
+    if (active) {
+      if (k >= a.max_depth) {
+        fin = true;  // depth <= 0
       } else {
-        const HitRec h = hit_record_of(geo[bi], inv_r[bi], bt, ox, oy, oz, dx, dy, dz);
-        const DevMaterial& m = a.mats[bi];
-        const int kind = m.kind;
-        double ndx, ndy, ndz;
-        bool ok = true;
+        ++rays;
+        pbi = world_hit_m<kBVH>(geo, a.n, bv, nodes, leaf_geo, leaf_idx, ox, oy, oz, dx, dy, dz,
+                                A, pbt);
+        if (pbi < 0) {
+          // sky (main.cc:46-48), then attenuation * (...) innermost first
+          const double y = (1.0 / __builtin_sqrt(A)) * dy;
+          const double t = 0.5 * (y + 1.0);
+          cr = (1.0 - t) * 1.0 + t * 0.5;
+          cg = (1.0 - t) * 1.0 + t * 0.7;
+          cb = (1.0 - t) * 1.0 + t * 1.0;
+          for (int e = np - 1; e >= 0; --e) {
+            const DevMaterial& m = a.mats[path[(size_t)e * ps]];
+            cr = m.albedo[0] * cr;
+            cg = m.albedo[1] * cg;
+            cb = m.albedo[2] * cb;
+          }
+          fin = true;
+        } else {
+          resolved = true;
+        }
+      }
+    }
+
+    // ---- scatter ----
+    if (resolved) {
+      const int bi = pbi;
+      const HitRec h = hit_record_of(geo[bi], inv_r[bi], pbt, ox, oy, oz, dx, dy, dz);
+      const DevMaterial& m = a.mats[bi];
+      const int kind = m.kind;
+      double ndx = 0.0, ndy = 0.0, ndz = 0.0;
+      bool ok = true;
+      if (kind == RT_MAT_DIELECTRIC) {
+        const double inv = 1.0 / __builtin_sqrt(A);
+        const double ux = inv * dx, uy = inv * dy, uz = inv * dz;
+        const double ratio = h.front ? (1.0 / m.ir) : m.ir;
+        const double ct = __builtin_fmin(((-ux) * h.nx + (-uy) * h.ny) + (-uz) * h.nz, 1.0);
+        const double st = __builtin_sqrt(1.0 - ct * ct);
+        // cannot_refract || reflectance(...) > random_double(): the draw is
+        // made only when refraction is possible
+        const bool reflect = ratio * st > 1.0 || reflectance(ct, ratio) > random_double(rng);
+        if (reflect) {  // reflect(v, n) = v - 2*dot(v,n)*n
+          const double dn = (ux * h.nx + uy * h.ny) + uz * h.nz;
+          ndx = ux - (2.0 * dn) * h.nx;
+          ndy = uy - (2.0 * dn) * h.ny;
+          ndz = uz - (2.0 * dn) * h.nz;
+        } else {  // refract(uv, n, ratio), cos_theta = ct
+          const double qx2 = ratio * (ux + ct * h.nx);
+          const double qy2 = ratio * (uy + ct * h.ny);
+          const double qz2 = ratio * (uz + ct * h.nz);
+          const double par =
+              -__builtin_sqrt(__builtin_fabs(1.0 - ((qx2 * qx2 + qy2 * qy2) + qz2 * qz2)));
+          ndx = qx2 + par * h.nx;
+          ndy = qy2 + par * h.ny;
+          ndz = qz2 + par * h.nz;
+        }
+      } else {
+        // random_in_unit_sphere() (vec3.h:83-95): trials of raw z, y, x draws
+        // (g++'s order, vec3.h:78-81) until one lies in the ball; lambertian
+        // and metal lanes share this one loop. (A look-ahead of trials generated
+        // a loop iteration ahead, as psrt_trace keeps, was measured 11% slower
+        // here: DESIGN.md §14.)
+        uint32_t rz, ry, rx;
+        for (;;) {
+          raw32_x3(rng, rz, ry, rx, rng);
+          if (in_unit_sphere_raw(rx, ry, rz)) break;
+        }
+        // random(-1, 1) of each draw, exact from the raw value (psrt_device.h)
+        const double x = pm1_raw(rx), y = pm1_raw(ry), z = pm1_raw(rz);
         if (kind == RT_MAT_LAMBERTIAN) {
           // normal + random_unit_vector(); the normal if that is near zero
-          double x, y, z;
-          in_unit_sphere(rng, x, y, z);
           const double inv = 1.0 / __builtin_sqrt((x * x + y * y) + z * z);
           ndx = h.nx + inv * x;
           ndy = h.ny + inv * y;
           ndz = h.nz + inv * z;
-          if (__builtin_fabs(ndx) < 1e-8 && __builtin_fabs(ndy) < 1e-8 && __builtin_fabs(ndz) < 1e-8)
+          if (__builtin_fabs(ndx) < 1e-8 && __builtin_fabs(ndy) < 1e-8 &&
+              __builtin_fabs(ndz) < 1e-8)
             ndx = h.nx, ndy = h.ny, ndz = h.nz;
         } else {
+          // metal: reflect(unit(d), n) + fuzz * random_in_unit_sphere();
+          // absorbed unless outward
           const double inv = 1.0 / __builtin_sqrt(A);
           const double ux = inv * dx, uy = inv * dy, uz = inv * dz;
-          bool reflect = true;
-          double ratio = 0.0, ct = 0.0;
-          if (kind == RT_MAT_DIELECTRIC) {
-            ratio = h.front ? (1.0 / m.ir) : m.ir;
-            ct = __builtin_fmin(((-ux) * h.nx + (-uy) * h.ny) + (-uz) * h.nz, 1.0);
-            const double st = __builtin_sqrt(1.0 - ct * ct);
-            // cannot_refract || reflectance(...) > random_double()
-            reflect = ratio * st > 1.0 || reflectance(ct, ratio) > random_double(rng);
-          }
-          if (reflect) {  // reflect(v, n) = v - 2*dot(v,n)*n
-            const double dn = (ux * h.nx + uy * h.ny) + uz * h.nz;
-            ndx = ux - (2.0 * dn) * h.nx;
-            ndy = uy - (2.0 * dn) * h.ny;
-            ndz = uz - (2.0 * dn) * h.nz;
-          } else {  // refract(uv, n, ratio), cos_theta = ct
-            const double qx = ratio * (ux + ct * h.nx);
-            const double qy = ratio * (uy + ct * h.ny);
-            const double qz = ratio * (uz + ct * h.nz);
-            const double par = -__builtin_sqrt(__builtin_fabs(1.0 - ((qx * qx + qy * qy) + qz * qz)));
-            ndx = qx + par * h.nx;
-            ndy = qy + par * h.ny;
-            ndz = qz + par * h.nz;
-          }
-          if (kind == RT_MAT_METAL) {  // + fuzz * random_in_unit_sphere(); absorbed unless outward
-            double x, y, z;
-            in_unit_sphere(rng, x, y, z);
-            ndx = ndx + m.fuzz * x;
-            ndy = ndy + m.fuzz * y;
-            ndz = ndz + m.fuzz * z;
-            ok = ((ndx * h.nx + ndy * h.ny) + ndz * h.nz) > 0.0;
-          }
+          const double dn = (ux * h.nx + uy * h.ny) + uz * h.nz;
+          ndx = (ux - (2.0 * dn) * h.nx) + m.fuzz * x;
+          ndy = (uy - (2.0 * dn) * h.ny) + m.fuzz * y;
+          ndz = (uz - (2.0 * dn) * h.nz) + m.fuzz * z;
+          ok = ((ndx * h.nx + ndy * h.ny) + ndz * h.nz) > 0.0;
         }
-        if (!ok) {
-          fin = true;
-        } else {
-          if (kind != RT_MAT_DIELECTRIC) path[(size_t)np++ * ps] = bi;
-          ox = h.px, oy = h.py, oz = h.pz;
-          dx = ndx, dy = ndy, dz = ndz;
-          A = (dx * dx + dy * dy) + dz * dz;
-          ++k;
-        }
+      }
+      if (!ok) {
+        fin = true;
+      } else {
+        if (kind != RT_MAT_DIELECTRIC) path[(size_t)np++ * ps] = bi;
+        ox = h.px, oy = h.py, oz = h.pz;
+        dx = ndx, dy = ndy, dz = ndz;
+        A = (dx * dx + dy * dy) + dz * dz;
+        ++k;
       }
     }
     if (fin) {
@@ -351,12 +391,14 @@ __global__ __launch_bounds__(kMatBlock) void psrt_trace_mat(const double4* __res
   }
 }
 
-template __global__ void psrt_trace_mat<false>(const double4* __restrict__,
-                                               const double* __restrict__, double* __restrict__,
-                                               MatArgs, BvhView);
-template __global__ void psrt_trace_mat<true>(const double4* __restrict__,
-                                              const double* __restrict__, double* __restrict__,
-                                              MatArgs, BvhView);
+#define PSRT_MAT_INSTANTIATE(B, L)                                                         \
+  template __global__ void psrt_trace_mat<B, L>(const double4* __restrict__,                \
+                                                const double* __restrict__, double* __restrict__, \
+                                                MatArgs, BvhView);
+PSRT_MAT_INSTANTIATE(false, false)
+PSRT_MAT_INSTANTIATE(true, false)
+PSRT_MAT_INSTANTIATE(true, true)
+#undef PSRT_MAT_INSTANTIATE
 
 // pixel_color += sample (main.cc:77-84) over colour records, in sample order;
 // write_color (color.h:8-24) on the last chunk. One lane per pixel; block 0
