@@ -71,6 +71,15 @@ if os.path.exists(trace):
     n1 = int(sys.argv[4]) if len(sys.argv) > 4 else 0
     if n1 and len(d) > n1:
         avg["average_ns_unpipelined"] = sum(d[-n1:]) / n1
+    # multi-frame launches (bench.py batches its timed frames, B per launch):
+    # the batched dispatches are the long ones; their duration per frame is
+    # what bench.py's roofline divides by (PSRT_FRAMES_PER_LAUNCH=B)
+    fpl = int(os.environ.get("PSRT_FRAMES_PER_LAUNCH", "1"))
+    if fpl > 1 and d:
+        long_ = [x for x in d if x >= 0.5 * max(d)]
+        avg["frames_per_launch"] = fpl
+        avg["batched_dispatches"] = len(long_)
+        avg["average_ns_per_frame_batched"] = sum(long_) / len(long_) / fpl
     avg["dispatch_ns"] = d
 fetch = c.get("FETCH_SIZE", 0.0) * 1024 * 2
 write = c.get("WRITE_SIZE", 0.0) * 1024
