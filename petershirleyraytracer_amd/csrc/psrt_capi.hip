@@ -670,7 +670,7 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
   int mat_grid = use_bvh ? c->grid_mat_bvh : c->grid_mat;
   unsigned mat_lds = 0;
   if (mat && use_bvh) {
-    const unsigned bytes = psrt::mat_lds_bytes(c->n_nodes, c->n_leaf);
+    const unsigned bytes = psrt::mat_lds_layout(c->n, c->n_nodes, c->n_leaf, c->n_big).bytes;
     int pc = 0;
     const char* ml = std::getenv("PSRT_MAT_LDS");
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, psrt::psrt_trace_mat<true, true>,

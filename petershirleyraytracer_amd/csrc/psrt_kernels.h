@@ -181,7 +181,7 @@ struct DevMaterial {
 };
 static_assert(sizeof(DevMaterial) == 48, "device material layout");
 #ifndef PSRT_MAT_BLOCK
-#define PSRT_MAT_BLOCK 320  // 5 waves: four workgroups (20 waves) per CU share 160 KB of LDS
+#define PSRT_MAT_BLOCK 512  // 8 waves: two workgroups per CU share 160 KB of LDS
 #endif
 constexpr int kMatBlock = PSRT_MAT_BLOCK;
 #ifndef PSRT_MAT_WAVES
@@ -214,11 +214,27 @@ struct MatArgs {
   unsigned path_stride;
 };
 
-// psrt_trace_mat<true, true> stages the BVH in dynamic LDS: nodes (2 float4
-// each, plus the padding node), leaf spheres, leaf indices; byte size:
-__host__ __device__ inline unsigned mat_lds_bytes(int n_nodes, int n_leaf) {
-  return 32u * (unsigned)(n_nodes + 1) + 32u * (unsigned)n_leaf +
-         ((4u * (unsigned)n_leaf + 15u) & ~15u);
+// psrt_trace_mat<true, true> stages the scene in dynamic LDS: BVH nodes (2
+// float4 each, plus the padding node), leaf spheres, spheres {c, r*r} and
+// 1/r by index, materials {albedo, fuzz or ir} and kinds by index, leaf
+// indices, big-sphere indices; byte offsets, 16-B aligned (book scene: 487
+// spheres, 71 KB; two 512-thread workgroups per CU)
+struct MatLdsLayout {
+  unsigned nodes, leaf_geo, geo, mat, inv, leaf_idx, kind, big, bytes;
+};
+__host__ __device__ inline MatLdsLayout mat_lds_layout(int n, int n_nodes, int n_leaf, int n_big) {
+  auto a16 = [](unsigned x) { return (x + 15u) & ~15u; };
+  MatLdsLayout l;
+  l.nodes = 0;
+  l.leaf_geo = 32u * (unsigned)(n_nodes + 1);
+  l.geo = l.leaf_geo + 32u * (unsigned)n_leaf;
+  l.mat = l.geo + 32u * (unsigned)n;
+  l.inv = l.mat + 32u * (unsigned)n;
+  l.leaf_idx = a16(l.inv + 8u * (unsigned)n);
+  l.kind = a16(l.leaf_idx + 4u * (unsigned)n_leaf);
+  l.big = a16(l.kind + 4u * (unsigned)n);
+  l.bytes = a16(l.big + 4u * (unsigned)(n_big > 0 ? n_big : 1));
+  return l;
 }
 
 template <bool kBVH, bool kLds>

@@ -77,7 +77,8 @@ __device__ __forceinline__ void test_sphere_m(const double4 s, int idx, double o
 // hittable_list::hit(r, 0.001, inf) for one lane.
 template <bool kBVH>
 __device__ __forceinline__ int world_hit_m(const double4* __restrict__ geo, int n,
-                                           const BvhView& bv, const float4* __restrict__ nodes,
+                                           const BvhView& bv, const int* __restrict__ big_idx,
+                                           const float4* __restrict__ nodes,
                                            const double4* __restrict__ leaf_geo,
                                            const int* __restrict__ leaf_idx, double ox, double oy, double oz,
                                            double dx, double dy, double dz, double A, double& bt) {
@@ -91,7 +92,7 @@ __device__ __forceinline__ int world_hit_m(const double4* __restrict__ geo, int 
     return bi;
   }
   for (int b = 0; b < bv.n_big; ++b) {
-    const int idx = bv.big_idx[b];
+    const int idx = big_idx[b];
     test_sphere_m(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
   }
   // Far origins are re-based at their root-box entry (as hit_traverse): the
@@ -153,23 +154,56 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
   const uint64_t total = a.total_units;
   int* const path = a.path + (size_t)blockIdx.x * kMatBlock + threadIdx.x;
   const size_t ps = a.path_stride;
-  // kLds: the BVH in dynamic LDS (mat_lds_bytes), so the walk's dependent
-  // node loads see LDS latency instead of L1 / L2 latency
+  // kLds: the scene in dynamic LDS (mat_lds_layout): the walk's dependent node
+  // loads and every per-hit lookup (sphere, 1/r, material) see LDS latency
+  // instead of L1 / L2 latency
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   const float4* __restrict__ nodes = bv.nodes;
   const double4* __restrict__ leaf_geo = bv.leaf_geo;
   const int* __restrict__ leaf_idx = bv.leaf_idx;
+  const int* __restrict__ big_idx = bv.big_idx;
+  const double4* __restrict__ lgeo = geo;
+  const double* __restrict__ linv = inv_r;
+  const double4* __restrict__ lmat = nullptr;  // kLds: {albedo, fuzz (metal) / ir (dielectric)}
+  const int* __restrict__ lkind = nullptr;
   if constexpr (kLds) {
-    float4* const sn = (float4*)s_dyn;
-    double4* const sg = (double4*)(s_dyn + 32u * (unsigned)(bv.n_nodes + 1));
-    int* const si = (int*)(s_dyn + 32u * (unsigned)(bv.n_nodes + 1) + 32u * (unsigned)bv.n_leaf);
+    const MatLdsLayout lay = mat_lds_layout(a.n, bv.n_nodes, bv.n_leaf, bv.n_big);
+    float4* const sn = (float4*)(s_dyn + lay.nodes);
+    double4* const slg = (double4*)(s_dyn + lay.leaf_geo);
+    double4* const sg = (double4*)(s_dyn + lay.geo);
+    double4* const sm = (double4*)(s_dyn + lay.mat);
+    double* const sv = (double*)(s_dyn + lay.inv);
+    int* const sli = (int*)(s_dyn + lay.leaf_idx);
+    int* const sk = (int*)(s_dyn + lay.kind);
+    int* const sb = (int*)(s_dyn + lay.big);
     for (int e = threadIdx.x; e < 2 * (bv.n_nodes + 1); e += kMatBlock) sn[e] = bv.nodes[e];
-    for (int e = threadIdx.x; e < bv.n_leaf; e += kMatBlock) sg[e] = bv.leaf_geo[e], si[e] = bv.leaf_idx[e];
+    for (int e = threadIdx.x; e < bv.n_leaf; e += kMatBlock) slg[e] = bv.leaf_geo[e], sli[e] = bv.leaf_idx[e];
+    for (int e = threadIdx.x; e < a.n; e += kMatBlock) {
+      const DevMaterial& m = a.mats[e];
+      sg[e] = geo[e];
+      sv[e] = inv_r[e];
+      sm[e] = make_double4(m.albedo[0], m.albedo[1], m.albedo[2],
+                           m.kind == RT_MAT_METAL ? m.fuzz : m.ir);
+      sk[e] = m.kind;
+    }
+    for (int e = threadIdx.x; e < bv.n_big; e += kMatBlock) sb[e] = bv.big_idx[e];
     __syncthreads();
-    nodes = sn;
-    leaf_geo = sg;
-    leaf_idx = si;
+    nodes = sn, leaf_geo = slg, leaf_idx = sli, big_idx = sb;
+    lgeo = sg, linv = sv, lmat = sm, lkind = sk;
   }
+  // material of sphere i: kind, albedo, fuzz / ir
+  constexpr bool kLm = kLds;
+  auto mat_kind = [&](int i) { return kLm ? lkind[i] : a.mats[i].kind; };
+  auto mat_albedo = [&](int i, double& r, double& g, double& b) {
+    if constexpr (kLm) {
+      const double4 m = lmat[i];
+      r = m.x, g = m.y, b = m.z;
+    } else {
+      r = a.mats[i].albedo[0], g = a.mats[i].albedo[1], b = a.mats[i].albedo[2];
+    }
+  };
+  auto mat_fuzz = [&](int i) { return kLm ? lmat[i].w : a.mats[i].fuzz; };
+  auto mat_ir = [&](int i) { return kLm ? lmat[i].w : a.mats[i].ir; };
 
   uint64_t win_base = 0;
   unsigned win_left = 0;
@@ -276,8 +310,8 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
         fin = true;  // depth <= 0
       } else {
         ++rays;
-        pbi = world_hit_m<kBVH>(geo, a.n, bv, nodes, leaf_geo, leaf_idx, ox, oy, oz, dx, dy, dz,
-                                A, pbt);
+        pbi = world_hit_m<kBVH>(lgeo, a.n, bv, big_idx, nodes, leaf_geo, leaf_idx, ox, oy, oz,
+                                dx, dy, dz, A, pbt);
         if (pbi < 0) {
           // sky (main.cc:46-48), then attenuation * (...) innermost first
           const double y = (1.0 / __builtin_sqrt(A)) * dy;
@@ -286,10 +320,11 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
           cg = (1.0 - t) * 1.0 + t * 0.7;
           cb = (1.0 - t) * 1.0 + t * 1.0;
           for (int e = np - 1; e >= 0; --e) {
-            const DevMaterial& m = a.mats[path[(size_t)e * ps]];
-            cr = m.albedo[0] * cr;
-            cg = m.albedo[1] * cg;
-            cb = m.albedo[2] * cb;
+            double ar, ag, ab;
+            mat_albedo(path[(size_t)e * ps], ar, ag, ab);
+            cr = ar * cr;
+            cg = ag * cg;
+            cb = ab * cb;
           }
           fin = true;
         } else {
@@ -301,15 +336,15 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
     // ---- scatter ----
     if (resolved) {
       const int bi = pbi;
-      const HitRec h = hit_record_of(geo[bi], inv_r[bi], pbt, ox, oy, oz, dx, dy, dz);
-      const DevMaterial& m = a.mats[bi];
-      const int kind = m.kind;
+      const HitRec h = hit_record_of(lgeo[bi], linv[bi], pbt, ox, oy, oz, dx, dy, dz);
+      const int kind = mat_kind(bi);
       double ndx = 0.0, ndy = 0.0, ndz = 0.0;
       bool ok = true;
       if (kind == RT_MAT_DIELECTRIC) {
         const double inv = 1.0 / __builtin_sqrt(A);
         const double ux = inv * dx, uy = inv * dy, uz = inv * dz;
-        const double ratio = h.front ? (1.0 / m.ir) : m.ir;
+        const double ir = mat_ir(bi);
+        const double ratio = h.front ? (1.0 / ir) : ir;
         const double ct = __builtin_fmin(((-ux) * h.nx + (-uy) * h.ny) + (-uz) * h.nz, 1.0);
         const double st = __builtin_sqrt(1.0 - ct * ct);
         // cannot_refract || reflectance(...) > random_double(): the draw is
@@ -358,9 +393,10 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
           const double inv = 1.0 / __builtin_sqrt(A);
           const double ux = inv * dx, uy = inv * dy, uz = inv * dz;
           const double dn = (ux * h.nx + uy * h.ny) + uz * h.nz;
-          ndx = (ux - (2.0 * dn) * h.nx) + m.fuzz * x;
-          ndy = (uy - (2.0 * dn) * h.ny) + m.fuzz * y;
-          ndz = (uz - (2.0 * dn) * h.nz) + m.fuzz * z;
+          const double fz = mat_fuzz(bi);
+          ndx = (ux - (2.0 * dn) * h.nx) + fz * x;
+          ndy = (uy - (2.0 * dn) * h.ny) + fz * y;
+          ndz = (uz - (2.0 * dn) * h.nz) + fz * z;
           ok = ((ndx * h.nx + ndy * h.ny) + ndz * h.nz) > 0.0;
         }
       }

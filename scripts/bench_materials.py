@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--height", type=int, default=800)
     ap.add_argument("--spp", type=int, default=10)
     ap.add_argument("--depth", type=int, default=50)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cpu-rows", type=int, default=8)
     ap.add_argument("--cpu-threads", type=int, default=0)
