@@ -29,8 +29,12 @@ def book(oracle_mod):
     return sp, mt, oracle_mod.camera_look_at_lens(aspect=1.5)
 
 
-@pytest.mark.parametrize("cull", [True, False])
-def test_book_scene_bit_exact(oracle_mod, book, cull):
+@pytest.mark.parametrize("cull,lds", [(True, None), (True, "0"), (False, None)])
+def test_book_scene_bit_exact(oracle_mod, book, cull, lds, monkeypatch):
+    """The culled kernel with the scene in LDS (default) and in global memory
+    (PSRT_MAT_LDS=0), and the linear scan."""
+    if lds is not None:
+        monkeypatch.setenv("PSRT_MAT_LDS", lds)
     sp, mt, lens = book
     W, H, spp, seed = 72, 48, 4, 9
     acc, rgb, st = P.render_materials(sp, mt, _lens(lens), W, H, spp, 50, seed, cull=cull)
