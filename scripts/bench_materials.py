@@ -73,9 +73,12 @@ def main():
         "steps": a.steps, "warmup": a.warmup, "dtype": "f64",
     }
     ctx.close()
-    # the C restatement on the host cores, a bounded sample of rows
+    # the C restatement on the host cores (the usable ones: affinity capped by
+    # the cgroup CPU quota), a bounded sample of rows; then one thread
     import oracle
-    threads = a.cpu_threads or len(os.sched_getaffinity(0))
+    from bench import host_cpus
+    hc = host_cpus()
+    threads = a.cpu_threads or hc["usable"]
     ol = oracle.camera_look_at_lens(aspect=W / H)
     osp, omt = oracle.scene_book_final(1)
     rows = a.cpu_rows
@@ -84,8 +87,16 @@ def main():
                                  threads=threads)
     dt = time.perf_counter() - t0
     n = oracle.rows_owned(H, 0, max(1, H // rows)) * W * S
+    t0 = time.perf_counter()
+    oracle.render_mat(osp, omt, ol, W, H, S, a.depth, 0, H // 2, H, threads=1)
+    dt1 = time.perf_counter() - t0
     out["cpu_baseline"] = {"value": n / (dt * 1e6), "unit": "Msamples/s", "cores": threads,
-                           "kind": "port", "sample": f"{n} samples ({n // (W * S)} rows)"}
+                           "kind": "port", "one_thread_value": W * S / (dt1 * 1e6),
+                           "nproc": hc["nproc"], "cgroup_cpu_quota": hc["cgroup_quota"],
+                           "cpu_model": hc["cpu_model"],
+                           "sample": f"{n} samples ({n // (W * S)} rows, C restatement "
+                                     f"oracle/rt_oracle_mat.c, {threads} threads); one thread: "
+                                     f"the middle row"}
     print(json.dumps(out))
 
 
