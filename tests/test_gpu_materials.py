@@ -111,3 +111,22 @@ def test_lens_radius_zero_and_no_cull_flag(oracle_mod):
     ref, _ = oracle_mod.render_mat(MIXED_SPHERES, MIXED_MATS, lens, W, H, spp, 50, 1, threads=8)
     assert np.array_equal(bits(a), bits(ref))
     assert FLAG_NO_CULL == 1
+
+
+def test_long_paths_between_mirrors(oracle_mod):
+    """Paths that use the path column deeply: two near-parallel mirror spheres
+    (r = 1e5, a gap of 1) with glass and diffuse balls between them; ~76 rays
+    per sample, some paths cut at depth 300; the same at depth 4096 (the
+    RT_FLAG_MATERIALS bound)."""
+    R = 1e5
+    sp = np.array([[0, -R - 0.5, 0, R], [0, R + 0.5, 0, R], [0.0, 0.0, -3.0, 0.25],
+                   [0.4, 0.1, -6.0, 0.3], [-0.5, -0.1, -9.0, -0.2]])
+    mt = np.array([[1, 0.98, 0.97, 0.96, 0.0, 0.0], [1, 0.97, 0.98, 0.99, 0.02, 0.0],
+                   [2, 1, 1, 1, 0.0, 1.5], [0, 0.7, 0.3, 0.2, 0, 0], [2, 1, 1, 1, 0, 1.5]])
+    lens = oracle_mod.camera_look_at_lens((0, 0, 0), (0, 0.05, -1), (0, 1, 0), 60.0, 4 / 3, 0.0,
+                                          1.0)
+    for depth in (300, 4096):
+        acc, _, st = P.render_materials(sp, mt, _lens(lens), 16, 12, 3, depth, 5)
+        ref, rays = oracle_mod.render_mat(sp, mt, lens, 16, 12, 3, depth, 5, threads=8)
+        assert np.array_equal(bits(acc), bits(ref)), depth
+        assert st["rays"] == rays and rays > 50 * 16 * 12 * 3
