@@ -853,6 +853,10 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
   // marked dirty, the enqueued part is fenced by ev_all1 like a whole render,
   // and the next render re-zeroes them with a stream-ordered memset first.
   c->dirty = true;
+  // test hook (tests/test_gpu_context.py): fail after chunk k's trace launch
+  // and before its reduce, as a HIP error there would
+  const char* fa = std::getenv("PSRT_FAIL_AFTER_TRACE");
+  const int fail_at = fa ? std::atoi(fa) : -1;
   auto enqueue_chunks = [&]() -> int {
   for (int ch = 0; ch < nchunks; ++ch) {
     const int s0 = (int)(ch * s_chunk);
@@ -938,6 +942,8 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
       stamps ? pick(T{}, T{}, F{}, c->grid_bvh) : pick(T{}, F{}, F{}, c->grid_bvh);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[2 * ch + 1], st));
+    if (ch == fail_at)
+      return set_error(RT_E_HIP, "PSRT_FAIL_AFTER_TRACE: failure injected after chunk %d", ch);
     // one psrt_reduce per frame; frame 0's also folds the launch's counter
     // sets into the render's totals and re-zeroes the queue heads
     for (size_t f = 0; f < nf; ++f) {

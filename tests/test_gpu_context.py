@@ -203,3 +203,31 @@ def test_multi_frame_launch_equals_single_frames(monkeypatch, buf_mb):
     with pytest.raises(RuntimeError):
         ctx.render_device_frames(prm, 33)
     ctx.close()
+
+
+@pytest.mark.parametrize("fail_at", ["0", "1"])
+def test_render_after_a_failure_mid_render(oracle_mod, monkeypatch, fail_at):
+    """A render that fails after a trace launch and before its reduce (the
+    PSRT_FAIL_AFTER_TRACE hook stands in for a HIP error there) leaves the
+    queue heads and counter sets non-zero: the context is marked dirty, and
+    the next render re-zeroes them first and is bit-exact with exact counts.
+    fail_at 1: the second of three sample chunks (1 MB sample buffer)."""
+    import torch
+    sph = oracle_mod.scene_random_spheres(1)
+    w, h, spp = 48, 32, 150
+    cam = oracle_mod.camera_look_at(aspect=w / h)
+    monkeypatch.setenv("PSRT_SAMPLE_BUF_MB", "1")  # 68 samples of 1536 pixels: chunks of 52, 52, 46
+    ctx = P.Context(0)
+    ctx.set_scene(sph, cam)
+    acc = torch.zeros((h, w, 3), dtype=torch.float64, device="cuda:0")
+    monkeypatch.setenv("PSRT_FAIL_AFTER_TRACE", fail_at)
+    with pytest.raises(RuntimeError):
+        ctx.render_device(P.params(w, h, spp, 50, 3), acc.data_ptr())
+    ctx.sync_stats()  # waits for the part that was enqueued
+    monkeypatch.delenv("PSRT_FAIL_AFTER_TRACE")
+    ctx.render_device(P.params(w, h, spp, 50, 3), acc.data_ptr())
+    st = ctx.sync_stats()
+    want, _, rays = oracle_mod.render(sph, cam, w, h, spp, 50, 3, threads=8)
+    assert np.array_equal(bits(acc.cpu().numpy()), bits(want))
+    assert st["rays"] == rays and st["samples"] == w * h * spp
+    ctx.close()
