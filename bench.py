@@ -321,7 +321,7 @@ def main():
     import torch.distributed as dist
 
     import petershirleyraytracer_amd as P
-    from petershirleyraytracer_amd.dist import gather_frame, rows_owned, shard
+    from petershirleyraytracer_amd.dist import gather_frame, gather_frames, rows_owned, shard
     from petershirleyraytracer_amd.render import (FLAG_CULL_STATS, FLAG_NO_CULL, FLAG_NO_FIXPOINT,
                                                   FLAG_NO_TAIL_PRIORITY)
 
@@ -409,7 +409,7 @@ def main():
     dev = torch.device("cuda", local)
     # per slot: B frames' accumulators and bytes
     acc = [torch.zeros((B, rows, w, 3), dtype=torch.float64, device=dev) for _ in range(depth)]
-    rgb = torch.zeros((h, w, 3), dtype=torch.uint8, device=dev) if rank == 0 and world > 1 else None
+    rgb = torch.zeros((h, w, 3), dtype=torch.uint8, device=dev) if rank == 0 and world > 1 else None  # --gather-fp64
     rgb_rows = [torch.zeros((B, rows, w, 3), dtype=torch.uint8, device=dev)
                 for _ in range(depth)] if world > 1 else None
     # every step ends with the frame's bytes in pinned host memory (rank 0):
@@ -457,15 +457,17 @@ def main():
             src = rgb_rows[sl]
         comm.wait_stream(st)
         with torch.cuda.stream(comm):
-            for f in range(nb):
-                fr = gather_frame(src[f], h, rank, world)
-                if rank == 0:
-                    if args.gather_fp64:
-                        ctxs[sl].quantize_device(fr.data_ptr(), w, h, spp, rgb.data_ptr(),
+            # the launch's nb frames in one gather (one collective, one
+            # de-interleave per rank), then to pinned host memory on rank 0
+            frs = gather_frames(src[:nb], h, rank, world)
+            if rank == 0:
+                if args.gather_fp64:
+                    for f in range(nb):
+                        ctxs[sl].quantize_device(frs[f].data_ptr(), w, h, spp, rgb.data_ptr(),
                                                  comm.cuda_stream)
-                    else:
-                        rgb.copy_(fr)
-                    host_rgb[sl][f].copy_(rgb, non_blocking=True)
+                        host_rgb[sl][f].copy_(rgb, non_blocking=True)
+                else:
+                    host_rgb[sl][:nb].copy_(frs, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(comm)
         pending[sl] = (is_timed, ev, nb)

@@ -31,23 +31,33 @@ def rows_owned(height: int, rank: int, world: int) -> int:
 
 def gather_frame(local: torch.Tensor, height: int, rank: int, world: int,
                  dst: int = 0) -> Optional[torch.Tensor]:
-    """Gather per-rank row blocks [rows_owned, W, C] into the full frame
-    [height, W, C] on rank `dst` (None elsewhere).
+    """One frame: `gather_frames` of a [rows_owned, W, C] block."""
+    if world == 1:
+        return local
+    out = gather_frames(local.unsqueeze(0), height, rank, world, dst)
+    return None if out is None else out[0]
 
-    One gather to `dst` of blocks padded to ceil(height/world) rows: only the
-    destination receives them (an all_gather would send every block to every
-    rank). A rank that owns no rows (world > height) sends an all-padding
-    block. The destination then de-interleaves."""
+
+def gather_frames(local: torch.Tensor, height: int, rank: int, world: int,
+                  dst: int = 0) -> Optional[torch.Tensor]:
+    """Gather per-rank row blocks [B, rows_owned, W, C] of B frames into the
+    full frames [B, height, W, C] on rank `dst` (None elsewhere).
+
+    One gather to `dst` of blocks padded to ceil(height/world) rows, for all B
+    frames at once (one collective and one de-interleave per rank instead of
+    one per frame): only the destination receives them (an all_gather would
+    send every block to every rank). A rank that owns no rows (world > height)
+    sends an all-padding block. The destination then de-interleaves."""
     if world == 1:
         return local
     max_rows = rows_owned(height, 0, world)
     mine = rows_owned(height, rank, world)
-    if local.shape[0] != mine:
-        raise ValueError(f"rank {rank} holds {local.shape[0]} rows, owns {mine}")
-    w, ch = local.shape[1], local.shape[2]
-    padded = local.new_zeros((max_rows, w, ch))
+    if local.dim() != 4 or local.shape[1] != mine:
+        raise ValueError(f"rank {rank} holds {tuple(local.shape)}, owns {mine} rows")
+    nb, w, ch = local.shape[0], local.shape[2], local.shape[3]
+    padded = local.new_zeros((nb, max_rows, w, ch))
     if mine:
-        padded[:mine] = local
+        padded[:, :mine] = local
     # gloo's gather takes host tensors only (the N > 1 rehearsal on one GPU
     # runs gloo over device frames): stage through host memory there
     host = dist.get_backend() == "gloo" and padded.device.type != "cpu"
@@ -58,9 +68,9 @@ def gather_frame(local: torch.Tensor, height: int, rank: int, world: int,
         parts = [p.to(local.device) for p in parts]
     if rank != dst:
         return None
-    frame = local.new_empty((height, w, ch))
+    frames = local.new_empty((nb, height, w, ch))
     for r in range(world):
         n = rows_owned(height, r, world)
         if n:
-            frame[r::world] = parts[r][:n]
-    return frame
+            frames[:, r::world] = parts[r][:, :n]
+    return frames

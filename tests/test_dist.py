@@ -30,7 +30,7 @@ def _worker(rank, world, port, w, h, spp, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import oracle as O
-    from petershirleyraytracer_amd.dist import gather_frame, rows_owned, shard
+    from petershirleyraytracer_amd.dist import gather_frame, gather_frames, rows_owned, shard
     off, stride = shard(rank, world)
     sph = O.scene_random_spheres(1)
     cam = O.camera_look_at(aspect=w / h)
@@ -43,11 +43,17 @@ def _worker(rank, world, port, w, h, spp, out_path):
     # bench.py's default N > 1 step: each rank quantises its rows (write_color
     # is per pixel) and only the uint8 rows are gathered
     frame8 = gather_frame(torch.from_numpy(np.ascontiguousarray(rgb)), h, rank, world)
+    # bench.py's multi-frame launches: a launch's frames in one gather (frame f
+    # here: the rows + f, so every frame differs)
+    batch = torch.stack([torch.from_numpy(np.ascontiguousarray(rgb)) + f for f in range(3)])
+    frames8 = gather_frames(batch, h, rank, world)
     if rank == 0:
         np.save(out_path, frame.numpy())
         np.save(out_path + ".rgb.npy", frame8.numpy())
+        for f in range(3):
+            assert np.array_equal(frames8[f].numpy(), frame8.numpy() + f)
     else:
-        assert frame is None and frame8 is None
+        assert frame is None and frame8 is None and frames8 is None
     dist.barrier()
     dist.destroy_process_group()
 
