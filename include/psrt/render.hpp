@@ -92,6 +92,37 @@ inline frame render(const hittable_list& world, const camera& cam, int width, in
   return f;
 }
 
+// The book's material integrator and thin lens (extension):
+// rt_render_materials over flattened spheres, one rt_material each.
+inline frame render_materials(const std::vector<rt_sphere>& spheres,
+                              const std::vector<rt_material>& mats, const rt_camera_lens& cam,
+                              int width, int height, int spp, int max_depth, uint64_t seed = 0,
+                              int row_offset = 0, int row_stride = 1) {
+  if (mats.size() != spheres.size())
+    throw std::runtime_error("render_materials: one material per sphere");
+  rt_params p{};
+  p.width = width;
+  p.height = height;
+  p.spp = spp;
+  p.max_depth = max_depth;
+  p.seed = seed;
+  p.row_offset = row_offset;
+  p.row_stride = row_stride;
+  p.flags = RT_FLAG_MATERIALS;
+  frame f;
+  f.width = width;
+  f.height = height;
+  f.spp = spp;
+  f.rows = rt_rows_owned(height, row_offset, row_stride);
+  if (f.rows < 0) f.rows = 0;
+  f.accum.resize((size_t)f.rows * width * 3);
+  f.rgb8.resize((size_t)f.rows * width * 3);
+  check(rt_render_materials(spheres.data(), mats.data(), (int)spheres.size(), &cam, &p,
+                            f.accum.data(), f.rgb8.data(), &f.stats),
+        "rt_render_materials");
+  return f;
+}
+
 // ---- scene files (rt_scene_load; DESIGN.md §Scene files) --------------------
 struct scene_file {
   std::vector<rt_sphere> spheres;  // hittable_list order

@@ -9,6 +9,8 @@
 //   raytracer --scene-file s.scene  # world/camera/parameters from a scene file;
 //                                   # flags given on the command line win
 //   raytracer --scene final --save-scene final.scene   # write the scene, render nothing
+//   raytracer --scene book --width 1200 --height 800 --spp 10 [--aperture 0.1 --focus 10]
+//                                   # the book's materials + thin lens
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -45,9 +47,9 @@ void random_spheres(hittable_list& world, unsigned seed) {
 
 int usage() {
   std::fprintf(stderr,
-               "raytracer [--scene two|final | --scene-file FILE] [--width W] [--height H]\n"
+               "raytracer [--scene two|final|book | --scene-file FILE] [--width W] [--height H]\n"
                "          [--spp S] [--depth D] [--seed N] [--rows OFF:STRIDE] [-o FILE] [--p6]\n"
-               "          [--accum FILE] [--save-scene FILE]\n");
+               "          [--accum FILE] [--save-scene FILE] [--aperture A] [--focus F]\n");
   return 2;
 }
 
@@ -57,6 +59,7 @@ int main(int argc, char** argv) {
   std::string scene = "two", out_path, accum_path, scene_path, save_path;
   int width = 400, height = -1, spp = 100, depth = 50, row_off = 0, row_stride = 1;
   unsigned long long seed = 0;
+  double aperture = 0.1, focus = 10.0;  // --scene book: the book's lens
   bool p6 = false, set_w = false, set_h = false, set_spp = false, set_depth = false,
        set_seed = false;
   for (int a = 1; a < argc; ++a) {
@@ -75,6 +78,8 @@ int main(int argc, char** argv) {
     else if (k == "--seed") seed = std::strtoull(v, nullptr, 10), set_seed = true;
     else if (k == "-o") out_path = v;
     else if (k == "--accum") accum_path = v;
+    else if (k == "--aperture") aperture = std::atof(v);
+    else if (k == "--focus") focus = std::atof(v);
     else if (k == "--rows") {
       if (std::sscanf(v, "%d:%d", &row_off, &row_stride) != 2) return usage();
     } else return usage();
@@ -108,6 +113,8 @@ int main(int argc, char** argv) {
     if (height < 0) height = (int)(width / cam.aspect_ratio);
     world.add(make_shared<sphere>(point3(0, 0, -1), 0.5));
     world.add(make_shared<sphere>(point3(0, -100.5, 0), 100.0));
+  } else if (scene == "book") {
+    if (height < 0) height = (int)(width / 1.5);
   } else if (scene == "final") {
     if (height < 0) height = (int)(width / 1.5);
     random_spheres(world, 1);
@@ -117,6 +124,10 @@ int main(int argc, char** argv) {
   }
 
   if (!save_path.empty()) {
+    if (scene == "book") {
+      std::cerr << "raytracer: scene files hold spheres only (no materials)\n";
+      return 2;
+    }
     try {
       rt_params p{};
       p.width = width;
@@ -136,8 +147,23 @@ int main(int argc, char** argv) {
 
   try {
     const auto t0 = std::chrono::steady_clock::now();
-    const psrt::frame f = psrt::render(world, cam, width, height, spp, depth, seed, row_off,
-                                       row_stride);
+    psrt::frame f;
+    if (scene == "book" && scene_path.empty()) {
+      // the book's random_scene() with materials, lookfrom (13,2,3), vfov 20
+      const int n = rt_scene_book_final(1, nullptr, nullptr, 0);
+      std::vector<rt_sphere> sph((size_t)n);
+      std::vector<rt_material> mats((size_t)n);
+      rt_scene_book_final(1, sph.data(), mats.data(), n);
+      const double from[3] = {13, 2, 3}, at[3] = {0, 0, 0}, up[3] = {0, 1, 0};
+      rt_camera_lens lc{};
+      psrt::check(rt_camera_look_at_lens(from, at, up, 20.0, (double)width / height, aperture,
+                                         focus, &lc),
+                  "rt_camera_look_at_lens");
+      f = psrt::render_materials(sph, mats, lc, width, height, spp, depth, seed, row_off,
+                                 row_stride);
+    } else {
+      f = psrt::render(world, cam, width, height, spp, depth, seed, row_off, row_stride);
+    }
     const double secs =
         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     std::ofstream file;

@@ -32,7 +32,7 @@ def main():
 
     import torch
     import petershirleyraytracer_amd as P
-    from petershirleyraytracer_amd.render import FLAG_MATERIALS, FLAG_NO_CULL
+    from petershirleyraytracer_amd.render import FLAG_CULL_STATS, FLAG_MATERIALS, FLAG_NO_CULL
 
     W, H, S = a.width, a.height, a.spp
     sp, mt = P.scene_book_final(1)
@@ -59,18 +59,40 @@ def main():
         kms.append(s["kernel_ms"])
         rays += s["rays"]
     step = sum(ms) / len(ms)
+    # one untimed frame of the counting variant: the sphere / box tests the
+    # kernel executes (deterministic: the same for every frame of a seed)
+    ctx.render_device(P.params(W, H, S, a.depth, 0, flags=flags | FLAG_CULL_STATS),
+                      acc.data_ptr(), rgb.data_ptr(), st)
+    cs = ctx.sync_stats()
+    kms = sum(kms) / len(kms)
+    # FP64-op slots as bench.py counts them for psrt_trace: 18 per exact sphere
+    # test, 7 per FP32 box test, ~61 per traced ray (hit record, scatter, draws)
+    ops = cs["tests_executed"] * 18 + cs["box_tests"] * 7 + cs["rays"] * 61
+    achieved = ops / (kms * 1e-3) / 1e12
+    roof = {"bound": "valu", "achieved": round(achieved, 4), "peak": 39.32, "unit": "TFLOP/s",
+            "frac": round(achieved / 39.32, 4), "traffic": None, "kernel": "psrt_trace_mat",
+            "avg_launch_ms": round(kms, 4), "executed_sphere_tests_per_launch": cs["tests_executed"],
+            "executed_box_tests_per_launch": cs["box_tests"], "rays_per_launch": cs["rays"],
+            "note": "FP64-op slots (tests x 18 + boxes x 7 + rays x 61) / kernel time, "
+                    "against 256 CU x 64 lanes x 2.4 GHz non-FMA FP64"}
+    pmc = os.path.join(ROOT, "profiles", "pmc_mat.json")
+    if os.path.exists(pmc):
+        d = json.load(open(pmc))
+        roof["valu_issue"] = {"simd_cycles_per_valu_inst": round(d.get("simd_cycles_per_valu", 0), 3),
+                              "wait_inst_frac": round(d.get("wait_inst_frac", 0), 3),
+                              "source": "profiles/pmc_mat.json"}
     out = {
         "metric": "Msamples/sec (materials extension, book final scene)",
         "value": W * H * S / (step * 1e3),
         "unit": "Msamples/s",
         "ms_per_step": step,
-        "kernel_ms": sum(kms) / len(kms),
+        "kernel_ms": kms,
         "grays_per_s": rays / (sum(ms) * 1e6),
         "rays_per_sample": rays / (a.steps * W * H * S),
         "config": {"scene": "book_final(seed 1), 487 spheres, lambertian/metal/dielectric",
                    "width": W, "height": H, "spp": S, "max_depth": a.depth,
                    "lens": "aperture 0.1, focus 10", "cull": not a.no_cull},
-        "steps": a.steps, "warmup": a.warmup, "dtype": "f64",
+        "steps": a.steps, "warmup": a.warmup, "dtype": "f64", "roofline": roof,
     }
     ctx.close()
     # the C restatement on the host cores (the usable ones: affinity capped by

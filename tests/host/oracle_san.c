@@ -16,6 +16,11 @@ int oracle_world_hit(const rt_sphere*, int, const double*, const double*, double
 int oracle_scene_random_spheres(unsigned, rt_sphere*, int);
 void oracle_camera_default(rt_camera*);
 void oracle_camera_look_at(const double*, const double*, const double*, double, double, rt_camera*);
+int oracle_render_mat(const rt_sphere*, const rt_material*, int, const rt_camera_lens*,
+                      const rt_params*, int, double*, unsigned long long*);
+int oracle_scene_book_final(unsigned, rt_sphere*, rt_material*, int);
+void oracle_camera_look_at_lens(const double*, const double*, const double*, double, double,
+                                double, double, rt_camera_lens*);
 
 static double acc1[40 * 24 * 3], acc2[40 * 24 * 3];
 static unsigned char rgb[40 * 24 * 3];
@@ -50,6 +55,21 @@ int main(void) {
       (void)oracle_world_hit(two, 2, o[k], d[k], 0.0, INFINITY, rec);
       (void)oracle_world_hit(fin, nf, o[k], d[k], 0.0, INFINITY, rec);
     }
+  }
+  { /* the materials extension (rt_oracle_mat.c): book scene, lens, depth edges */
+    static rt_sphere bs[600];
+    static rt_material bm[600];
+    rt_camera_lens lc;
+    const int nb = oracle_scene_book_final(1, bs, bm, 600);
+    oracle_camera_look_at_lens(from, at, up, 20.0, 40.0 / 24.0, 0.1, 10.0, &lc);
+    p.max_depth = 50, p.row_offset = 0, p.row_stride = 1, p.spp = 2;
+    bad |= oracle_render_mat(bs, bm, nb, &lc, &p, 3, acc1, &rays) != 0;
+    bad |= oracle_render_mat(bs, bm, nb, &lc, &p, 1, acc2, &rays) != 0;
+    bad |= memcmp(acc1, acc2, sizeof acc1) != 0;
+    p.max_depth = 4096, p.spp = 1;
+    bad |= oracle_render_mat(bs, bm, nb, &lc, &p, 2, acc1, &rays) != 0;
+    p.max_depth = 4097;
+    bad |= oracle_render_mat(bs, bm, nb, &lc, &p, 2, acc1, &rays) != RT_E_INVALID;
   }
   printf(bad ? "FAIL\n" : "ok\n");
   return bad;

@@ -156,6 +156,27 @@ int main(int argc, char** argv) {
     corpus.push_back(t);
     CHECK(parse_roundtrip(t) == nf, "final scene round trip");
   }
+  // the book's scene with materials and the lens camera (host helpers of the
+  // materials extension): NULL outputs, truncating caps, degenerate lenses
+  {
+    const int nb = rt_scene_book_final(1, nullptr, nullptr, 0);
+    CHECK(nb == 487, "book scene count");
+    std::vector<rt_sphere> bs((size_t)nb);
+    std::vector<rt_material> bm((size_t)nb);
+    CHECK(rt_scene_book_final(1, bs.data(), bm.data(), nb) == nb, "book scene");
+    CHECK(rt_scene_book_final(7, bs.data(), nullptr, 10) == rt_scene_book_final(7, nullptr, nullptr, 0),
+          "book scene truncated");
+    for (int k = 0; k < nb; ++k)
+      CHECK(bm[k].kind >= RT_MAT_LAMBERTIAN && bm[k].kind <= RT_MAT_DIELECTRIC, "material kind");
+    const double from[3] = {13, 2, 3}, at[3] = {0, 0, 0}, up[3] = {0, 1, 0};
+    rt_camera_lens lc{};
+    CHECK(rt_camera_look_at_lens(from, at, up, 20.0, 1.5, 0.1, 10.0, &lc) == RT_OK, "lens camera");
+    CHECK(rt_camera_look_at_lens(from, at, up, 20.0, 1.5, -1.0, 10.0, &lc) == RT_E_INVALID,
+          "negative aperture");
+    CHECK(rt_camera_look_at_lens(from, at, up, 20.0, 1.5, 0.1, 0.0, &lc) == RT_E_INVALID,
+          "zero focus distance");
+    (void)rt_camera_look_at_lens(from, from, up, 20.0, 1.5, 0.1, 1.0, &lc);  // lookfrom == lookat
+  }
   // mutation fuzz: byte flips, deletions, insertions of grammar tokens and
   // random bytes, truncation, duplication of lines
   const int iters = 6000;

@@ -58,5 +58,6 @@ def test_oracle_restatement_under_sanitizers(tmp_path):
     exe = str(tmp_path / "oracle_san")
     subprocess.run(["gcc", *SAN, "-std=c99", "-Wall", "-Wno-unused-function", "-ffp-contract=off",
                     "-pthread", "-o", exe, os.path.join(ROOT, "tests", "host", "oracle_san.c"),
-                    os.path.join(ROOT, "oracle", "rt_oracle.c"), "-lm"], check=True)
+                    os.path.join(ROOT, "oracle", "rt_oracle.c"),
+                    os.path.join(ROOT, "oracle", "rt_oracle_mat.c"), "-lm"], check=True)
     assert _run(exe).strip() == "ok"
