@@ -161,12 +161,6 @@ struct rt_context {
   rt_camera_lens lcam{};
   int* d_path = nullptr;  // per resident lane, its path's attenuating hits
   size_t path_cap = 0;    // ints
-  // camera-ray candidate lists through the lens (psrt_mat_camera_lists),
-  // cached per (materials / lens camera, W, H, row_offset, row_stride)
-  uint4* d_mat_plist = nullptr;
-  size_t mat_plist_cap = 0;  // records
-  bool mat_plist_valid = false;
-  int mat_plist_key[4] = {0, 0, 0, 0};
   rt_stats last{};
   int n_last = 0;
 };
@@ -331,7 +325,6 @@ int rt_context_destroy(rt_context* c) {
   (void)hipFree(c->d_nb_items);
   (void)hipFree(c->d_mats);
   (void)hipFree(c->d_path);
-  (void)hipFree(c->d_mat_plist);
   for (auto e : c->ev) (void)hipEventDestroy(e);
   if (c->ev_all0) (void)hipEventDestroy(c->ev_all0);
   if (c->ev_all1) (void)hipEventDestroy(c->ev_all1);
@@ -360,7 +353,6 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
   }
   c->scene.clear();  // set again once every structure is built
   c->has_mats = false;  // materials belong to the scene they were set for
-  c->mat_plist_valid = false;
   const int cap = n > 0 ? n : 1;
   if (cap > c->n_cap) {
     (void)hipFree(c->d_geo);
@@ -819,23 +811,6 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     c->plist_cap = P;
     c->plist_valid = false;
   }
-  // the material integrator's camera-ray lists through the lens: the same
-  // conditions, for the lens camera's origin
-  const double lom = std::max(std::fabs(c->lcam.base.origin[0]),
-                              std::max(std::fabs(c->lcam.base.origin[1]),
-                                       std::fabs(c->lcam.base.origin[2])));
-  const bool mat_list = mat && use_bvh && c->n < (int)psrt::kCamOverflow && lom <= c->r_check &&
-                        !std::getenv("PSRT_NO_CAMLIST");
-  if (mat_list && c->mat_plist_cap < P) {
-    rc = quiesce(c);
-    if (rc) return rc;
-    (void)hipFree(c->d_mat_plist);
-    c->d_mat_plist = nullptr;
-    c->mat_plist_cap = 0;
-    HIP_TRY(hipMalloc(&c->d_mat_plist, P * sizeof(uint4)));
-    c->mat_plist_cap = P;
-    c->mat_plist_valid = false;
-  }
   if (c->dirty) {  // an earlier render failed part-way: heads and sets back to zero
     HIP_TRY(hipMemsetAsync(c->d_counters + kHeads, 0,
                            (kCounterWords - kHeads) * sizeof(unsigned long long), st));
@@ -872,35 +847,6 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     std::copy(key, key + 4, c->plist_key);
     c->plist_valid = true;
     bv.plist = c->d_plist;
-  }
-  if (mat_list) {
-    if (!(c->mat_plist_valid && std::equal(key, key + 4, c->mat_plist_key))) {
-      psrt::MatCamListArgs la{};
-      for (int k = 0; k < 3; ++k) {
-        la.org[k] = c->lcam.base.origin[k];
-        la.llc[k] = c->lcam.base.lower_left[k];
-        la.hor[k] = c->lcam.base.horizontal[k];
-        la.ver[k] = c->lcam.base.vertical[k];
-      }
-      la.lens_radius = std::fabs(c->lcam.lens_radius);
-      la.width = p->width;
-      la.height = p->height;
-      la.row_offset = p->row_offset;
-      la.row_stride = p->row_stride;
-      la.rows = rows;
-      la.leaf_geo = c->d_leaf_geo;
-      la.leaf_idx = c->d_leaf_idx;
-      la.n_leaf = c->n_leaf;
-      la.pad = c->pad;
-      la.plist = c->d_mat_plist;
-      const dim3 lg((p->width + psrt::kCamTile - 1) / psrt::kCamTile,
-                    (rows + psrt::kCamTile - 1) / psrt::kCamTile);
-      hipLaunchKernelGGL(psrt::psrt_mat_camera_lists, lg, dim3(64), 0, st, la);
-      HIP_TRY(hipGetLastError());
-      std::copy(key, key + 4, c->mat_plist_key);
-      c->mat_plist_valid = true;
-    }
-    ma.plist = c->d_mat_plist;
   }
   // A HIP failure after the first trace launch would leave the queue heads and
   // counter sets non-zero (only psrt_reduce re-zeroes them): the context is
@@ -1247,7 +1193,6 @@ int rt_context_set_materials(rt_context* c, const rt_material* mats, int n,
   }
   c->lcam = *cam;
   c->has_mats = true;
-  c->mat_plist_valid = false;
   return RT_OK;
 }
 
