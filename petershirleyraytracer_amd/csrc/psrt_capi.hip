@@ -717,6 +717,8 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     ma.mats = c->d_mats;
     ma.path = c->d_path;
     ma.path_stride = (unsigned)lanes;
+    const char* mb = std::getenv("PSRT_MAT_BATCH");  // tuning knob
+    ma.batch = mb ? (unsigned)std::max(1, std::atoi(mb)) : 48u;  // 40-56 best (profiles/r03_mat)
   }
 
   psrt::TraceArgs ta{};

@@ -212,6 +212,7 @@ struct MatArgs {
   // path[k * path_stride + lane slot], k < max_depth
   int* __restrict__ path;
   unsigned path_stride;
+  unsigned batch;  // parked lanes that trigger a batched BVH walk
 };
 
 // psrt_trace_mat<true, true> stages the scene in dynamic LDS: BVH nodes (2

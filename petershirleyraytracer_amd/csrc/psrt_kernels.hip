@@ -277,96 +277,6 @@ __device__ __forceinline__ bool test_sphere(const double4 s, int idx, double ox,
   return true;
 }
 
-// Point query for a short segment [o, o + bt*d] (the common case: the ray
-// re-hit the sphere it starts on at t ~ 0). Returns the list (psrt_bvh.h
-// GridHost: a cell, or the 2x2x2 block of cells the segment crosses into)
-// whose spheres are the only BVH spheres the segment can hit, kGridOutside
-// when the segment lies outside the grid (no BVH sphere can be hit), or
-// kGridNone when it cannot be bounded this way (the BVH must be walked).
-constexpr int kGridNone = -1, kGridOutside = -2;
-
-// The uniform constants hit_quick / the walk read on every ray. psrt_trace
-// keeps them in LDS and re-reads them per use (an LDS read issues on the LDS
-// pipe); held in SGPRs across the loop they spill, and each reload from the
-// spill lane is a VALU v_readlane (~20 per grid query).
-struct GridC {
-  float glo[3], ghi[3], ginv, gmargin;
-  int gdims[3], ncell;
-  // cell-index form of the widened segment bounds: fma(min, ginv, a0[k]) =
-  // (min - m - glo) ginv and fma(max, ginv, a1[k]) = (max + m - glo) ginv, up
-  // to FP32 rounding (~2^-24 of the coordinates, far inside the margin m)
-  float a0[3], a1[3];
-  int top[3], pad_;
-  double r_check, nb_c2;
-};
-
-__device__ __forceinline__ GridC grid_consts(const BvhView& bv) {
-  GridC g;
-  for (int k = 0; k < 3; ++k) {
-    g.glo[k] = bv.glo[k], g.ghi[k] = bv.ghi[k], g.gdims[k] = bv.gdims[k];
-    g.a0[k] = -(bv.glo[k] + bv.gmargin) * bv.ginv;
-    g.a1[k] = -(bv.glo[k] - bv.gmargin) * bv.ginv;
-    g.top[k] = bv.gdims[k] - 1;
-  }
-  g.ncell = bv.gdims[0] * bv.gdims[1] * bv.gdims[2];
-  g.ginv = bv.ginv;
-  g.gmargin = bv.gmargin;
-  g.pad_ = 0;
-  g.r_check = bv.r_check;
-  g.nb_c2 = bv.nb_c2;
-  return g;
-}
-
-
-// floor(x) as int, saturating (NaN -> 0): one v_cvt_flr_i32_f32
-__device__ __forceinline__ int cvt_flr_i32(float x) {
-  int r;
-  asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
-  return r;
-}
-
-// min(max(x, 0), hi): one v_med3_i32
-__device__ __forceinline__ int clamp0_i32(int x, int hi) {
-  int r;
-  asm("v_med3_i32 %0, %1, 0, %2" : "=v"(r) : "v"(x), "v"(hi));
-  return r;
-}
-
-__device__ __forceinline__ int grid_locate(const GridC& bv, double ox, double oy, double oz,
-                                           double dx, double dy, double dz, double bt) {
-  if (!(bt < 1e30)) return kGridNone;
-  // FP32 is enough within the caller's range guard: the test is conservative
-  // and its error is inside pad + margin (psrt_bvh.cpp, hit_quick)
-  const float o3[3] = {(float)ox, (float)oy, (float)oz};
-  const float d3[3] = {(float)dx, (float)dy, (float)dz};
-  const float tb = (float)bt * 1.00000048f;
-  int ci[3];
-  bool outside = false, ok = true, one = true;
-  // Cell range [c0, c1] of the widened segment per axis, from saturating
-  // floor-converts (huge coordinates saturate, and the caller's range guard
-  // keeps NaN out). Outside the grid when c1 < 0 or c0 > top on some axis:
-  // the widened bound then lies below glo / at or past the grid's far side
-  // (up to rounding far inside the margin), where no padded sphere box
-  // reaches. Then clipped to the grid: a hit point lies in a padded sphere
-  // box, hence in a cell of the grid.
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const float e = __builtin_fmaf(tb, d3[k], o3[k]);
-    const int r0 = cvt_flr_i32(__builtin_fmaf(fminf(o3[k], e), bv.ginv, bv.a0[k]));
-    const int r1 = cvt_flr_i32(__builtin_fmaf(fmaxf(o3[k], e), bv.ginv, bv.a1[k]));
-    const int top = bv.top[k];
-    outside = outside || r1 < 0 || r0 > top;
-    const int c0 = clamp0_i32(r0, top), c1 = clamp0_i32(r1, top);
-    ok = ok && c1 - c0 <= 1;
-    one = one && c1 == c0;
-    ci[k] = c0;
-  }
-  if (outside) return kGridOutside;
-  if (!ok) return kGridNone;
-  // one cell: its list; two cells on some axis: the 2x2x2 block list from ci
-  const int cell = (ci[2] * bv.gdims[1] + ci[1]) * bv.gdims[0] + ci[0];
-  return one ? cell : cell + bv.ncell;
-}
 
 
 // A per-lane counter that counts nothing: the sphere / box test counters of

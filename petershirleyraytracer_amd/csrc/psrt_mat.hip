@@ -84,38 +84,67 @@ __device__ __forceinline__ void test_sphere_m(const double4 s, int idx, double o
   }
 }
 
-// hittable_list::hit(r, 0.001, inf) for one lane.
+// hittable_list::hit(r, 0.001, inf) for one lane, cheap part: the big
+// spheres, then the point-location grid for the segment [o, o + bt d] (as
+// psrt_trace's hit_quick: a sphere with an accepted root t <= bt has its hit
+// point on that segment and inside its padded box, hence in a cell the segment
+// crosses; tmin = 0.001 only removes roots). Returns true when the closest hit
+// is decided (bt, bi); false when the BVH must be walked from (bt, bi).
 template <bool kBVH, bool kCount>
-__device__ __forceinline__ int world_hit_m(TestCount<kCount>& nt, TestCount<kCount>& nb,const double4* __restrict__ geo, int n,
-                                           const BvhView& bv, const int* __restrict__ big_idx,
-                                           const float4* __restrict__ nodes,
-                                           const double4* __restrict__ leaf_geo,
-                                           const int* __restrict__ leaf_idx, double ox, double oy,
-                                           double oz, double dx, double dy, double dz, double A,
-                                           double& bt) {
+__device__ __forceinline__ bool hit_quick_m(TestCount<kCount>& nt, const double4* __restrict__ geo,
+                                            int n, const BvhView& bv,
+                                            const int* __restrict__ big_idx, const GridC& gc,
+                                            double ox, double oy, double oz, double dx, double dy,
+                                            double dz, double A, double& bt, int& bi) {
   bt = __builtin_inf();
-  int bi = -1;
+  bi = -1;
   const double am = __builtin_fmax(__builtin_fabs(ox),
                                    __builtin_fmax(__builtin_fabs(oy), __builtin_fabs(oz)));
   // unbounded arithmetic or no BVH: the reference scan, verbatim
   if (!kBVH || !(A > 0.0 && A < 1e200) || !(am < 1e200)) {
     for (int i = 0; i < n; ++i) test_sphere_m(geo[i], i, ox, oy, oz, dx, dy, dz, A, bt, bi);
     nt.add((unsigned)n);
-    return bi;
+    return true;
   }
   for (int b = 0; b < bv.n_big; ++b) {
     const int idx = big_idx[b];
     test_sphere_m(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
   }
   nt.add((unsigned)bv.n_big);
-  // Far origins are re-based at their root-box entry (as hit_traverse): the
-  // FP32 slab test then sees coordinates of the scene's scale.
-  double t0 = 0.0;
-  if (!(am <= bv.r_check)) {
-    const double e = root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt);
-    if (e < 0.0) return bi;  // the segment [0, bt] misses every BVH sphere's padded box
-    t0 = e;
+  // FP32 grid query, exact within 256 S (psrt_trace hit_quick)
+  const double rg = 4.0 * gc.r_check;
+  const int cell = (am <= rg && (bt * bt) * A <= rg * rg)
+                       ? grid_locate(gc, ox, oy, oz, dx, dy, dz, bt) : kGridNone;
+  if (cell == kGridOutside) return true;  // no BVH sphere in [0, bt]
+  if (cell >= 0) {
+    const int e0 = bv.cell_start[cell], e1 = bv.cell_start[cell + 1];
+    for (int e = e0; e < e1; ++e) {
+      const int idx = bv.cell_items[e];
+      test_sphere_m(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
+    }
+    nt.add((unsigned)(e1 - e0));
+    return true;
   }
+  // far origin: the segment [0, bt] against the padded root box (FP64)
+  if (!(am <= bv.r_check) && root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt) < 0.0) return true;
+  return false;
+}
+
+// The BVH walk (stackless skip links) continuing from hit_quick_m's (bt, bi).
+template <bool kCount>
+__device__ __forceinline__ void hit_walk_m(TestCount<kCount>& nt, TestCount<kCount>& nb,
+                                           const BvhView& bv, const float4* __restrict__ nodes,
+                                           const double4* __restrict__ leaf_geo,
+                                           const int* __restrict__ leaf_idx, double ox, double oy,
+                                           double oz, double dx, double dy, double dz, double A,
+                                           double& bt, int& bi) {
+  const double am = __builtin_fmax(__builtin_fabs(ox),
+                                   __builtin_fmax(__builtin_fabs(oy), __builtin_fabs(oz)));
+  // Far origins are re-based at their root-box entry (as hit_traverse): the
+  // FP32 slab test then sees coordinates of the scene's scale (hit_quick_m
+  // has shown the entry exists)
+  double t0 = 0.0;
+  if (!(am <= bv.r_check)) t0 = __builtin_fmax(0.0, root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt));
   const float fox = (float)(ox + t0 * dx), foy = (float)(oy + t0 * dy), foz = (float)(oz + t0 * dz);
   const float ix = safe_inv((float)dx), iy = safe_inv((float)dy), iz = safe_inv((float)dz);
   const float oix = fox * ix, oiy = foy * iy, oiz = foz * iz;
@@ -147,7 +176,6 @@ __device__ __forceinline__ int world_hit_m(TestCount<kCount>& nt, TestCount<kCou
     nt.add((unsigned)cnt);
     tmax = tmax_up(bt - t0);
   }
-  return bi;
 }
 
 // Schlick's approximation (book ch. 10.4), pow(x, 5) as (x*x)*(x*x)*x
@@ -206,6 +234,10 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
     nodes = sn, leaf_geo = slg, leaf_idx = sli, big_idx = sb;
     lgeo = sg, linv = sv, lmat = sm, lkind = sk;
   }
+  // the grid constants hit_quick_m reads, in LDS (re-read per use, as psrt_trace)
+  __shared__ GridC s_gc;
+  if (threadIdx.x == 0) s_gc = grid_consts(bv);
+  __syncthreads();
   // material of sphere i: kind, albedo, fuzz / ir
   constexpr bool kLm = kLds;
   auto mat_kind = [&](int i) { return kLm ? lkind[i] : a.mats[i].kind; };
@@ -231,6 +263,12 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
   uint64_t rng = 0;   // the sample's stream: position of its next draw
   unsigned su = 0;
   unsigned long long rays = 0;
+  // Rays the grid cannot decide park (pending) with their partial (pbt, pbi)
+  // and are walked together once a.batch lanes wait or nothing else can move
+  // (psrt_trace's batched walk): the walk then runs for many lanes at once.
+  bool pending = false;
+  int pbi = -1;
+  double pbt = 0.0;
   TestCount<kCount> ntests, nboxes;  // RT_FLAG_CULL_STATS: executed sphere / box tests
 
   for (;;) {
@@ -317,35 +355,51 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
     if (__ballot(active) == 0) break;
 
     // ---- world.hit(r, 0.001, inf) of this bounce (book ch. 9-10) ----
-    bool fin = false, resolved = false;
-    int pbi = -1;
-    double pbt = 0.0;
+    bool fin = false, resolved = false, decided = false;
     double cr = 0.0, cg = 0.0, cb = 0.0;  // black: depth exhausted or absorbed
-    if (active) {
+    if (active && !pending) {
       if (k >= a.max_depth) {
         fin = true;  // depth <= 0
       } else {
         ++rays;
-        pbi = world_hit_m<kBVH>(ntests, nboxes, lgeo, a.n, bv, big_idx, nodes, leaf_geo,
-                                leaf_idx, ox, oy, oz, dx, dy, dz, A, pbt);
-        if (pbi < 0) {
-          // sky (main.cc:46-48), then attenuation * (...) innermost first
-          const double y = (1.0 / __builtin_sqrt(A)) * dy;
-          const double t = 0.5 * (y + 1.0);
-          cr = (1.0 - t) * 1.0 + t * 0.5;
-          cg = (1.0 - t) * 1.0 + t * 0.7;
-          cb = (1.0 - t) * 1.0 + t * 1.0;
-          for (int e = np - 1; e >= 0; --e) {
-            double ar, ag, ab;
-            mat_albedo(path[(size_t)e * ps], ar, ag, ab);
-            cr = ar * cr;
-            cg = ag * cg;
-            cb = ab * cb;
-          }
-          fin = true;
-        } else {
-          resolved = true;
+        unsigned zg = 0;
+        asm volatile("" : "+v"(zg));  // re-read the grid constants from LDS here
+        const GridC& gc = *(const GridC*)((const char*)&s_gc + zg);
+        decided = hit_quick_m<kBVH>(ntests, lgeo, a.n, bv, big_idx, gc, ox, oy, oz, dx, dy, dz,
+                                    A, pbt, pbi);
+        pending = !decided;
+      }
+    }
+    if constexpr (kBVH) {
+      const uint64_t pend = __ballot(pending);
+      if (pend != 0 && ((unsigned)__popcll(pend) >= a.batch ||
+                        __ballot(active && !pending && !fin) == 0)) {
+        if (pending) {
+          hit_walk_m(ntests, nboxes, bv, nodes, leaf_geo, leaf_idx, ox, oy, oz, dx, dy, dz, A,
+                     pbt, pbi);
+          pending = false;
+          decided = true;
         }
+      }
+    }
+    if (decided) {
+      if (pbi < 0) {
+        // sky (main.cc:46-48), then attenuation * (...) innermost first
+        const double y = (1.0 / __builtin_sqrt(A)) * dy;
+        const double t = 0.5 * (y + 1.0);
+        cr = (1.0 - t) * 1.0 + t * 0.5;
+        cg = (1.0 - t) * 1.0 + t * 0.7;
+        cb = (1.0 - t) * 1.0 + t * 1.0;
+        for (int e = np - 1; e >= 0; --e) {
+          double ar, ag, ab;
+          mat_albedo(path[(size_t)e * ps], ar, ag, ab);
+          cr = ar * cr;
+          cg = ag * cg;
+          cb = ab * cb;
+        }
+        fin = true;
+      } else {
+        resolved = true;
       }
     }
 
