@@ -766,20 +766,8 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     c->wave_log_used = need / 5;
   }
   {
-    const char* e = std::getenv("PSRT_BATCH");  // tuning knob (default 24 of 64 lanes)
-    ta.batch = e ? (unsigned)std::atoi(e) : 24u;
-    if (ta.batch < 1) ta.batch = 1;
-    const char* f = std::getenv("PSRT_RNG_FILL");  // tuning knob (default 2)
-    ta.rng_fill = f ? std::atoi(f) : 2;
-    if (ta.rng_fill < 1) ta.rng_fill = 1;
-    const char* x = std::getenv("PSRT_RNG_EXTRA");  // tuning knob (default 1, then defer)
-    ta.rng_extra = x ? std::atoi(x) : 1;
-    if (ta.rng_extra < 0) ta.rng_extra = 0;
-    const char* r = std::getenv("PSRT_REFILL_MIN");  // tuning knob (default 16 of 64 lanes)
-    ta.refill_min = r ? (unsigned)std::atoi(r) : 16u;
-    if (ta.refill_min < 1) ta.refill_min = 1;
-    const char* wt = std::getenv("PSRT_WALK_TAIL");  // tuning knob (default 4 lanes)
-    ta.walk_tail = wt ? (unsigned)std::atoi(wt) : 4u;
+    // (the loop schedule: kRefillMin, kWalkBatch, kWalkTail, kRngFill,
+    // kRngExtra in psrt_kernels.hip, compile-time since r03)
     // The kernel's per-lane counters are 32-bit; a lane flushes them in its
     // wave's refill block once one reaches flush_at, and between two such
     // blocks it adds at most one sample's work: <= max_depth + 1 rays (so

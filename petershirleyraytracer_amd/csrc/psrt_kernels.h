@@ -94,11 +94,6 @@ struct TraceArgs {
   unsigned long long* wave_log;     // diagnostic build: per wave {start, queue empty, exit,
                                     // iterations at queue empty, at exit} (s_memrealtime,
                                     // 100 MHz), or nullptr
-  unsigned batch;                   // parked lanes that trigger a batched BVH pass
-  int rng_fill;                     // look-ahead trials per lane per iteration (min)
-  int rng_extra;                    // extra trials while a scattering lane has none queued
-  unsigned refill_min;              // idle lanes that trigger the finish + refill block
-  unsigned walk_tail;               // a BVH pass stops once this few lanes still walk
   FastDiv div_s, div_w, div_p;      // unit / s_count, q / width, (f * pixels + q) / pixels
   unsigned flush_at;                // per-lane counters flush to the totals at this value
   int tail_prio;                    // raise the issue priority of waves whose queue is empty

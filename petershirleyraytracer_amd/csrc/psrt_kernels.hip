@@ -40,6 +40,14 @@ constexpr int kHitPrio = 2;
 constexpr int kTailPrio = 1;
 // Minimum waves per SIMD asked of the register allocator (80 VGPRs).
 constexpr int kTraceWaves = 6;
+// Loop schedule (tuned; re-swept under multi-frame launches in r03,
+// profiles/r03_knobs): compile-time constants, so they take no SGPRs in the
+// loop (held as kernel arguments they pushed SGPRs into VGPR-lane spills).
+constexpr unsigned kRefillMin = 16;  // idle lanes that trigger the finish + refill block
+constexpr unsigned kWalkBatch = 24;  // parked lanes that trigger a batched BVH pass
+constexpr unsigned kWalkTail = 4;    // a BVH pass stops once this few lanes still walk
+constexpr int kRngFill = 2;          // look-ahead trials per lane per iteration (min)
+constexpr int kRngExtra = 1;         // extra trials while a scattering lane has none queued
 
 __device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
 
@@ -106,6 +114,10 @@ struct SectionClock {
 };
 
 struct RefillConst {
+  // guided work queue phases (TraceArgs::ph_*), read when a wave takes a ticket
+  uint64_t ph_first[kQueuePhases + 1];
+  uint64_t ph_base[kQueuePhases];
+  unsigned ph_size[kQueuePhases];
   double cam[12];  // origin, lower_left, horizontal, vertical
   double wm1, hm1;  // (double)(W - 1), (double)(H - 1)   main.cc:80-81
   uint64_t seedmix[kMaxFrames];  // splitmix64(seed of frame f) (TraceArgs::frames)
@@ -609,6 +621,11 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
                             : threadIdx.x < 9 ? a.hor[threadIdx.x - 6]
                                               : a.ver[threadIdx.x - 9];
   if (threadIdx.x < kMaxFrames) s_rc.seedmix[threadIdx.x] = a.seedmix[threadIdx.x];
+  if (threadIdx.x <= kQueuePhases) s_rc.ph_first[threadIdx.x] = a.ph_first[threadIdx.x];
+  if (threadIdx.x < kQueuePhases) {
+    s_rc.ph_base[threadIdx.x] = a.ph_base[threadIdx.x];
+    s_rc.ph_size[threadIdx.x] = a.ph_size[threadIdx.x];
+  }
   if (threadIdx.x == 0) {
     s_rc.wm1 = (double)(a.width - 1);
     s_rc.hm1 = (double)(a.height - 1);
@@ -687,7 +704,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
     // for the few iterations they sit idle.
     const bool need = !active;
     const uint64_t need_mask = __ballot(need);
-    const bool run_block = need_mask != 0 && ((unsigned)__popcll(need_mask) >= a.refill_min ||
+    const bool run_block = need_mask != 0 && ((unsigned)__popcll(need_mask) >= kRefillMin ||
                                               need_mask == __ballot(1));
     if (run_block) {
       // The per-lane counters are 32-bit. Between two runs of this block a lane
@@ -730,6 +747,9 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
       uint64_t nb = 0;
       unsigned wsize = kWorkChunk;
       if (cnt > win_left) {
+        unsigned zq = 0;
+        asm volatile("" : "+v"(zq));  // the phases are re-read from LDS here
+        const RefillConst& rq = *(const RefillConst*)((const char*)&s_rc + zq);
         // sharded heads (psrt_kernels.h kQueues): this block's own head first,
         // then the next ones once it has run past the end of the work
         for (unsigned qnext = 0;; ++qnext) {
@@ -738,9 +758,9 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
           if (lane == 0) tk = atomicAdd(a.work_counter + kShardStride * h, 1ull);
           tk = __shfl(tk, 0) * kQueues + h;  // global ticket
           int ph = 0;
-          while (ph < kQueuePhases - 1 && tk >= a.ph_first[ph + 1]) ++ph;
-          nb = a.ph_base[ph] + (tk - a.ph_first[ph]) * a.ph_size[ph];
-          wsize = a.ph_size[ph];
+          while (ph < kQueuePhases - 1 && tk >= rq.ph_first[ph + 1]) ++ph;
+          nb = rq.ph_base[ph] + (tk - rq.ph_first[ph]) * rq.ph_size[ph];
+          wsize = rq.ph_size[ph];
           if (nb < total || qnext == kQueues - 1) break;
         }
       }
@@ -863,13 +883,13 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
     if constexpr (kBVH) {
       const uint64_t pend = __ballot(pending);
       const uint64_t movable = __ballot(active && !pending);
-      if (pend != 0 && ((unsigned)__popcll(pend) >= a.batch || movable == 0)) {
+      if (pend != 0 && ((unsigned)__popcll(pend) >= kWalkBatch || movable == 0)) {
         __builtin_amdgcn_s_setprio(kWalkPrio);
         if (pending) {
           clk.util(kUWalk);
           hit_traverse<kStamps, kLds>(bv, nodes, lleaf, lgeo, hint, ox, oy,
                                                          oz, dx, dy, dz, A, pbt, pbi, cs, wnode,
-                                                         movable ? a.walk_tail : 0u);
+                                                         movable ? kWalkTail : 0u);
           if (wnode >= bv.n_nodes) {
             pending = false;
             resolved = true;
@@ -922,8 +942,8 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
         qv1 = qv1 || to1;
         qv0 = qv0 || to0;
         ++f;
-      } while (f < a.rng_fill ||
-               (f < a.rng_fill + a.rng_extra &&
+      } while (f < kRngFill ||
+               (f < kRngFill + kRngExtra &&
                 __ballot(want && !qv0) != 0));
     }
     clk.mark(kSecFillShade);
