@@ -499,7 +499,6 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
     const uint64_t walking = __ballot(node < bv.n_nodes);
     if (walking == 0 || (tail && (unsigned)__popcll(walking) <= tail)) break;
     while (node < bv.n_nodes && leaf < 0) {
-      if (tail && (unsigned)__popcll(__ballot(1)) <= tail) break;  // test the held leaves
       if constexpr (kDiag) {
         if (first_active_lane()) ++cs.wave_trips;
       }
