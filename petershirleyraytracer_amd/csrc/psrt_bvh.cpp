@@ -332,6 +332,30 @@ BvhHost build_bvh(const rt_sphere* s, int n) {
     out.nb_word[j] = ((int32_t)out.nb_items.size() << 4) | (int32_t)nb.size();
     out.nb_items.insert(out.nb_items.end(), nb.begin(), nb.end());
   }
+
+  // inline records (BvhHost::cell_rec / nb_rec): slot 0 the count, slots
+  // 1.. the indices, in list order
+  auto pack = [](const int32_t* it, int cnt, int cap, uint32_t* w, int words) {
+    bool fits = cnt <= cap;
+    for (int e = 0; e < cnt && fits; ++e) fits = it[e] >= 0 && it[e] < (int32_t)kListOverflow;
+    uint16_t slot[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    slot[0] = fits ? (uint16_t)cnt : (uint16_t)kListOverflow;
+    for (int e = 0; fits && e < cnt; ++e) slot[e + 1] = (uint16_t)it[e];
+    for (int k = 0; k < words; ++k) w[k] = slot[2 * k] | (uint32_t)slot[2 * k + 1] << 16;
+  };
+  const size_t nlist = g.start.size() - 1;
+  out.cell_rec.assign(4 * nlist, 0u);
+  for (size_t c = 0; c < nlist; ++c)
+    pack(g.items.data() + g.start[c], g.start[c + 1] - g.start[c], kListRecMax,
+         &out.cell_rec[4 * c], 4);
+  out.nb_rec.assign(2 * (size_t)n, 0u);
+  for (int j = 0; j < n; ++j) {
+    const int32_t w = out.nb_word[j];
+    if (w < 0)
+      pack(nullptr, kNbRecMax + 1, kNbRecMax, &out.nb_rec[2 * (size_t)j], 2);  // no list
+    else
+      pack(out.nb_items.data() + (w >> 4), w & 15, kNbRecMax, &out.nb_rec[2 * (size_t)j], 2);
+  }
   out.enabled = true;
   return out;
 }

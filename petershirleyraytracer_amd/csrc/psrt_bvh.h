@@ -51,6 +51,9 @@ constexpr double kBigRatio = 16.0;   // radius > 16 x median -> tested every ray
 #endif
 constexpr int kLeafMax = PSRT_LEAF_MAX;
 constexpr int kNbMax = 15;           // neighbour lists longer than this use the grid
+constexpr int kListRecMax = 7;       // items of an inline grid-list record (BvhHost::cell_rec)
+constexpr int kNbRecMax = 3;         // items of an inline neighbour record (BvhHost::nb_rec)
+constexpr uint32_t kListOverflow = 0xFFFFu;
 
 // Point-location grid over the same padded boxes: cell -> spheres whose padded
 // box overlaps the cell. A ray whose segment [o, o + closest*d] lies inside one
@@ -81,6 +84,14 @@ struct BvhHost {
   // kNbMax); -1 for big spheres and spheres with more neighbours (grid path).
   std::vector<int32_t> nb_word;   // [n], by original index
   std::vector<int32_t> nb_items;  // original indices
+  // The same lists as inline records, the form psrt_trace reads (one load per
+  // query, no per-item loads): {count | i0 << 16, i1 | i2 << 16, ...} in
+  // uint16 slots. cell_rec: 4 words per grid list (up to kListRecMax items);
+  // nb_rec: 2 words per sphere (up to kNbRecMax). count = kListOverflow when
+  // the list is longer, an index does not fit 16 bits, or (nb_rec) sphere j
+  // has no neighbour list: the ray then takes the grid / the BVH walk.
+  std::vector<uint32_t> cell_rec;  // [2 * ncell][4]
+  std::vector<uint32_t> nb_rec;    // [n][2]
   double pad = 0.0;               // absolute box padding
   double r_check = 0.0;           // rays with |o|_inf > r_check use the linear sweep
   int depth = 0;

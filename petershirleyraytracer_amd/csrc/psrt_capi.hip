@@ -108,6 +108,8 @@ struct rt_context {
   int* d_cell_items = nullptr;
   int* d_nb_word = nullptr;
   int* d_nb_items = nullptr;
+  uint4* d_cell_rec = nullptr;  // grid lists as inline records (BvhHost::cell_rec)
+  uint2* d_nb_rec = nullptr;    // neighbour lists as inline records (BvhHost::nb_rec)
   std::vector<rt_sphere> scene;   // the scene the structures were built for
   psrt::GridHost pgrid;  // point-location grid (host copy of the geometry)
   double pad = 0.0;
@@ -323,6 +325,8 @@ int rt_context_destroy(rt_context* c) {
   (void)hipFree(c->d_cell_items);
   (void)hipFree(c->d_nb_word);
   (void)hipFree(c->d_nb_items);
+  (void)hipFree(c->d_cell_rec);
+  (void)hipFree(c->d_nb_rec);
   (void)hipFree(c->d_mats);
   (void)hipFree(c->d_path);
   for (auto e : c->ev) (void)hipEventDestroy(e);
@@ -393,9 +397,12 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
   (void)hipFree(c->d_cell_items);
   (void)hipFree(c->d_nb_word);
   (void)hipFree(c->d_nb_items);
+  (void)hipFree(c->d_cell_rec);
+  (void)hipFree(c->d_nb_rec);
   c->d_nodes = nullptr, c->d_leaf_geo = nullptr, c->d_leaf_idx = nullptr, c->d_big = nullptr;
   c->d_cell_start = nullptr, c->d_cell_items = nullptr;
   c->d_nb_word = nullptr, c->d_nb_items = nullptr;
+  c->d_cell_rec = nullptr, c->d_nb_rec = nullptr;
   c->bvh = b.enabled;
   c->n_nodes = c->n_big = c->n_leaf = 0;
   if (b.enabled) {
@@ -437,6 +444,12 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
     if (nw) HIP_TRY(up(c->d_nb_word, b.nb_word.data(), nw * sizeof(int)));
     if (!b.nb_items.empty())
       HIP_TRY(up(c->d_nb_items, b.nb_items.data(), b.nb_items.size() * sizeof(int)));
+    HIP_TRY(hipMalloc(&c->d_cell_rec, std::max<size_t>(4, b.cell_rec.size()) * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&c->d_nb_rec, std::max<size_t>(2, b.nb_rec.size()) * sizeof(uint32_t)));
+    if (!b.cell_rec.empty())
+      HIP_TRY(up(c->d_cell_rec, b.cell_rec.data(), b.cell_rec.size() * sizeof(uint32_t)));
+    if (!b.nb_rec.empty())
+      HIP_TRY(up(c->d_nb_rec, b.nb_rec.data(), b.nb_rec.size() * sizeof(uint32_t)));
     // the uploads above read host vectors of this block: wait for them here
     HIP_TRY(hipStreamSynchronize(c->stream));
   }
@@ -462,6 +475,8 @@ static psrt::BvhView bvh_view(const rt_context* c) {
   v.cell_items = c->d_cell_items;
   v.nb_word = c->d_nb_word;
   v.nb_items = c->d_nb_items;
+  v.cell_rec = c->d_cell_rec;
+  v.nb_rec = c->d_nb_rec;
   v.nb_c2 = 0.25 * c->pad * c->pad;
   if (std::getenv("PSRT_NO_NEIGHBORS")) v.nb_c2 = -1.0;  // A/B knob: C^2 <= -r^2 never holds
   // grid bounds / scale in FP32, as used: the cell index of the device is a

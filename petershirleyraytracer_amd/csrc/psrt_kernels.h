@@ -30,7 +30,7 @@ constexpr int kQueues = PSRT_QUEUES;
 constexpr int kShardStride = 16;       // u64 words between heads / counter sets (128 B)
 // Scene data psrt_trace stages in (dynamic) LDS per workgroup: BVH nodes (2
 // float4 each, plus the padding node), spheres {c, r*r}, 1/r, leaf slots and
-// neighbour words; byte offsets, 16-B aligned. The host stages them when as
+// neighbour records (8 B); byte offsets, 16-B aligned. The host stages them when as
 // many workgroups per CU stay resident as without (C3: 573 nodes, 485
 // spheres, 41.6 KB; three workgroups).
 struct LdsLayout {
@@ -44,7 +44,7 @@ __host__ __device__ inline LdsLayout lds_layout(int n, int n_nodes, int n_leaf) 
   l.inv = l.geo + 32u * (unsigned)n;
   l.leaf = a16(l.inv + 8u * (unsigned)n);
   l.nb = a16(l.leaf + 4u * (unsigned)n_leaf);
-  l.bytes = a16(l.nb + 4u * (unsigned)n);
+  l.bytes = a16(l.nb + 8u * (unsigned)n);  // nb: BvhView::nb_rec
   return l;
 }
 
@@ -128,6 +128,11 @@ struct BvhView {
   const int* __restrict__ nb_word;
   const int* __restrict__ nb_items;
   double nb_c2;  // (pad/2)^2: C <= 0 or C^2 <= nb_c2 * r^2 puts o in j's padded ball
+  // the grid lists and neighbour lists as inline records (psrt_bvh.h
+  // BvhHost::cell_rec / nb_rec, the plist format): psrt_trace's hit_quick
+  // reads one record per query instead of an offset pair and the items
+  const uint4* __restrict__ cell_rec;  // [2 * ncell]
+  const uint2* __restrict__ nb_rec;    // [n]
 };
 
 constexpr int kCamTile = 8;         // camera-list tiles are 8 x 8 pixels (one wave)

@@ -340,7 +340,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
                                           double oz, double dx, double dy, double dz, double A,
                                           double& bt, int& bi, CS& cs, Clock& clk,
                                           bool& trapped, unsigned q,
-                                          const int* __restrict__ lnb, const GridC& gc) {
+                                          const uint2* __restrict__ lnb, const GridC& gc) {
   bt = __builtin_inf();
   bi = -1;
   trapped = false;
@@ -352,9 +352,11 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     bi = sweep_linear(geo, n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), bt);
     return true;
   }
-  bool fix = false, full = false;
-  int nbw = -1;
-  // camera ray: the pixel's candidate list (psrt_camera_lists), loaded early
+  bool fix = false, full = false, nb = false;
+  // The candidate list as an inline record {count | i0 << 16, i1 | i2 << 16,
+  // ...} (uint16 slots, count kListOverflow = none): a camera ray's pixel list
+  // (psrt_camera_lists), loaded early; the hint sphere's neighbour record or
+  // the grid list's replace it below.
   uint4 rec = make_uint4(kCamOverflow, 0u, 0u, 0u);
   if (hint < 0 && bv.plist) rec = bv.plist[q];
   if (hint >= 0) {
@@ -375,8 +377,11 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     // has its hit point there and within the root error of its own surface,
     // so its centre lies within r_j + r_k + pad of c_j: it is j's neighbour.
     if (bi == hint && am <= gc.r_check && gc.nb_c2 >= 0.0 &&
-        (ch <= 0.0 || ch * ch <= gc.nb_c2 * sh.w))
-      nbw = lnb[hint];
+        (ch <= 0.0 || ch * ch <= gc.nb_c2 * sh.w)) {
+      const uint2 nr = lnb[hint];
+      nb = (nr.x & 0xFFFFu) != kCamOverflow;
+      if (nb) rec = make_uint4(nr.x, nr.y, 0u, 0u);
+    }
   }
   clk.mark(kSecQHint);
   for (int b = 0; b < bv.n_big; ++b) {
@@ -388,21 +393,15 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
   // The candidate list of this ray, one of:
   //   neighbour list of the hint sphere (nb path), the pixel's camera list,
   //   or the grid cell holding [o, o + bt d];
-  // all three are walked by ONE loop below, so a wave whose lanes took
-  // different paths runs max(count) sphere tests instead of their sum.
-  const int* __restrict__ items = bv.nb_items;
-  int cnt = 0;
+  // all three are records of the same form, walked by ONE loop below, so a
+  // wave whose lanes took different paths runs max(count) sphere tests
+  // instead of their sum, and no trip loads anything but the sphere.
   bool listed = true;
-  const unsigned ncand = rec.x & 0xFFFFu;
-  const bool cam = nbw < 0 && ncand != kCamOverflow;
-  uint64_t lo = rec.x | (uint64_t)rec.y << 32, hi = rec.z | (uint64_t)rec.w << 32;
-  if (nbw >= 0) {
+  if (nb) {
     clk.util(kUNb);
-    items += nbw >> 4;
-    cnt = nbw & 15;
-  } else if (cam) {  // every BVH sphere a ray of this pixel can hit is listed
+  } else if ((rec.x & 0xFFFFu) != kCamOverflow) {
+    // every BVH sphere a ray of this pixel can hit is listed
     clk.util(kUCam);
-    cnt = (int)ncand;
   } else {
     clk.util(kUGrid);
     // FP32 query, exact while its error (~4 ulp of the segment's coordinates)
@@ -418,21 +417,20 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     else if (bt < 1e30) clk.util(kUGridNoneFin);
     else clk.util(kUGridNoneInf);
     if (cell >= 0) {
-      const int e0 = bv.cell_start[cell];
-      items = bv.cell_items + e0;
-      cnt = bv.cell_start[cell + 1] - e0;
+      rec = bv.cell_rec[cell];
+      // a list too long for a record: the walk decides (exact either way)
+      if ((rec.x & 0xFFFFu) == kCamOverflow) listed = false;
+    } else {
+      rec.x = 0u;
     }
   }
+  const int cnt = listed ? (int)(rec.x & 0xFFFFu) : 0;
+  uint64_t lo = rec.x | (uint64_t)rec.y << 32, hi = rec.z | (uint64_t)rec.w << 32;
   for (int e = 0; e < cnt; ++e) {
     clk.util(kUListTrip);
-    int idx;
-    if (cam) {
-      lo = (lo >> 16) | (hi << 48);
-      hi >>= 16;
-      idx = (int)(lo & 0xFFFFu);
-    } else {
-      idx = items[e];
-    }
+    lo = (lo >> 16) | (hi << 48);
+    hi >>= 16;
+    const int idx = (int)(lo & 0xFFFFu);
     if (idx == hint) continue;
     full |= test_sphere(lgeo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
   }
@@ -557,7 +555,7 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
   SectionClock<false> noclk;
   const GridC gc = grid_consts(bv);
   if (!hit_quick(geo, geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs, noclk, trapped,
-                 0u, bv.nb_word, gc))
+                 0u, bv.nb_rec, gc))
   {
     int node = 0;
     hit_traverse<false, false>(bv, bv.nodes, bv.leaf_idx, geo, hint, ox, oy, oz, dx, dy, dz, A,
@@ -604,7 +602,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
   double4* const s_geo = (double4*)(s_dyn + lay.geo);
   double* const s_inv = (double*)(s_dyn + lay.inv);
   int* const s_leaf = (int*)(s_dyn + lay.leaf);
-  int* const s_nb = (int*)(s_dyn + lay.nb);
+  uint2* const s_nb = (uint2*)(s_dyn + lay.nb);
   // Constants only the refill block reads (camera basis, image size, the
   // divisions' magic numbers, the seed) live in LDS and are re-read on every
   // refill through an offset the compiler cannot see through: held across
@@ -641,14 +639,14 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
     for (int e = threadIdx.x; e < 2 * (bv.n_nodes + 1); e += blockDim.x) s_nodes[e] = bv.nodes[e];
     for (int e = threadIdx.x; e < a.n; e += blockDim.x) s_geo[e] = geo[e], s_inv[e] = inv_r[e];
     for (int e = threadIdx.x; e < bv.n_leaf; e += blockDim.x) s_leaf[e] = bv.leaf_idx[e];
-    for (int e = threadIdx.x; e < a.n; e += blockDim.x) s_nb[e] = bv.nb_word[e];
+    for (int e = threadIdx.x; e < a.n; e += blockDim.x) s_nb[e] = bv.nb_rec[e];
   }
   __syncthreads();
   const float4* __restrict__ nodes = kLds ? s_nodes : bv.nodes;
   const double4* __restrict__ lgeo = kLds ? s_geo : geo;
   const double* __restrict__ linv = kLds ? s_inv : inv_r;
   const int* __restrict__ lleaf = kLds ? s_leaf : bv.leaf_idx;
-  const int* __restrict__ lnb = kLds ? s_nb : bv.nb_word;
+  const uint2* __restrict__ lnb = kLds ? s_nb : bv.nb_rec;
 
   // wave-uniform work window
   uint64_t win_base = 0;

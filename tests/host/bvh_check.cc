@@ -131,6 +131,31 @@ static void check_scene(const std::vector<rt_sphere>& s) {
     for (int e = 0; e < (int)want.size(); ++e)
       CHECK(b.nb_items[(w >> 4) + e] == want[e], "neighbour list = all spheres in reach, sorted");
   }
+  // inline records (what psrt_trace reads): slot 0 the count, then the list
+  // in order; kListOverflow exactly when the list does not fit
+  auto slots = [](const uint32_t* w, int words, int k) { return (int)((w[k / 2] >> (16 * (k % 2))) & 0xFFFFu); };
+  CHECK(b.cell_rec.size() == 4 * (g.start.size() - 1), "one record per grid list");
+  for (size_t c = 0; c + 1 < g.start.size(); ++c) {
+    const int cnt = g.start[c + 1] - g.start[c];
+    const uint32_t* w = &b.cell_rec[4 * c];
+    if (cnt > psrt::kListRecMax) {
+      CHECK(slots(w, 4, 0) == (int)psrt::kListOverflow, "long grid lists overflow their record");
+      continue;
+    }
+    CHECK(slots(w, 4, 0) == cnt, "grid record count");
+    for (int e = 0; e < cnt; ++e) CHECK(slots(w, 4, e + 1) == g.items[g.start[c] + e], "grid record items");
+  }
+  CHECK(b.nb_rec.size() == 2 * (size_t)n, "one neighbour record per sphere");
+  for (int j = 0; j < n; ++j) {
+    const int w = b.nb_word[j];
+    const uint32_t* r = &b.nb_rec[2 * (size_t)j];
+    if (w < 0 || (w & 15) > psrt::kNbRecMax) {
+      CHECK(slots(r, 2, 0) == (int)psrt::kListOverflow, "neighbour record overflow = grid path");
+      continue;
+    }
+    CHECK(slots(r, 2, 0) == (w & 15), "neighbour record count");
+    for (int e = 0; e < (w & 15); ++e) CHECK(slots(r, 2, e + 1) == b.nb_items[(w >> 4) + e], "neighbour record items");
+  }
   std::printf("ok %d %zu %zu %zu\n", m, b.big_idx.size(), ncell, g.items.size());
 }
 
