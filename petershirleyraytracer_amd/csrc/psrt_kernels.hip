@@ -120,6 +120,7 @@ struct RefillConst {
   unsigned ph_size[kQueuePhases];
   double cam[12];  // origin, lower_left, horizontal, vertical
   double wm1, hm1;  // (double)(W - 1), (double)(H - 1)   main.cc:80-81
+  double rwm1, rhm1;  // RN(1 / wm1), RN(1 / hm1), or 0 when the divisor is 0 (div_by)
   uint64_t seedmix[kMaxFrames];  // splitmix64(seed of frame f) (TraceArgs::frames)
   FastDiv div_s, div_w, div_p;
   int hm1_i, row_offset, row_stride, s_begin, frames;
@@ -128,6 +129,21 @@ struct RefillConst {
 __device__ __forceinline__ unsigned fast_div(unsigned n, const FastDiv& f) {
   const unsigned t = __umulhi(f.m, n);
   return (t + ((n - t) >> f.sh1)) >> f.sh2;
+}
+
+// x / d, correctly rounded, for x >= 0 and d >= 1 from y = RN(1/d) (the
+// camera ray's u and v, main.cc:80-81): q0 = RN(x y) is within 1.5 ulp of
+// x/d; one correction q1 = RN(q0 + RN(x - d q0) y) brings it within
+// 0.5 + 2^-50 ulp; with q1 within 1 ulp, r1 = x - d q1 is exact and
+// RN(q1 + r1 y) = RN(x/d) (Markstein's theorem). No intermediate under- or
+// overflows for these operands (x < 2^31, d < 2^31); x = 0 gives +0. Five
+// FP64 ops instead of the division's ten and a v_rcp_f64.
+__device__ __forceinline__ double div_by(double x, double d, double y) {
+  double q = x * y;
+  double r = __builtin_fma(-q, d, x);
+  q = __builtin_fma(r, y, q);
+  r = __builtin_fma(-q, d, x);
+  return __builtin_fma(r, y, q);
 }
 
 __device__ __forceinline__ unsigned mbcnt64(uint64_t m) {
@@ -264,6 +280,7 @@ __device__ __forceinline__ int sweep_linear(const double4* __restrict__ geo, int
 // Returns false when the pre-reject decided the sphere, true when the full
 // test ran. *c_out (if given) receives C = amc.amc - r^2 as sphere.cc:11 forms it.
 
+template <bool kPre = true>
 __device__ __forceinline__ bool test_sphere(const double4 s, int idx, double ox, double oy,
                                             double oz, double dx, double dy, double dz,
                                             double A, double& best_t, int& best_i,
@@ -271,7 +288,7 @@ __device__ __forceinline__ bool test_sphere(const double4 s, int idx, double ox,
   const double ax = ox - s.x, ay = oy - s.y, az = oz - s.z;
   const double c = ((ax * ax + ay * ay) + az * az) - s.w;
   if (c_out) *c_out = c;
-  if (c > 0.0 && best_t < 1e100) {
+  if (kPre && c > 0.0 && best_t < 1e100) {
     const double c2 = c * c, k2 = 2.0 * (c + 2.0 * s.w);
     if (c2 >= 0x1p-34 * (c + s.w) * k2 && (best_t * best_t) * A * k2 * (1.0 + 0x1p-4) < c2)
       return false;
@@ -363,7 +380,8 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     clk.util(kUHint);
     const double4 sh = lgeo[hint];
     double ch;
-    test_sphere(sh, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, &ch);
+    // the ray's first test: bt = +inf, so no pre-reject
+    test_sphere<false>(sh, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, &ch);
     fix = bv.fixpoint && ch == 0.0 && sh.w >= 0x1p-700 && sh.w <= 0x1p700 && am <= 0x1p40;
     ++cs.spheres;
     if (bi == hint) {
@@ -626,6 +644,8 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
   if (threadIdx.x == 0) {
     s_rc.wm1 = (double)(a.width - 1);
     s_rc.hm1 = (double)(a.height - 1);
+    s_rc.rwm1 = a.width > 1 ? 1.0 / s_rc.wm1 : 0.0;
+    s_rc.rhm1 = a.height > 1 ? 1.0 / s_rc.hm1 : 0.0;
     s_rc.div_s = a.div_s;
     s_rc.div_w = a.div_w;
     s_rc.div_p = a.div_p;
@@ -724,7 +744,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
         double tt = 0.0;
         unsigned short kk = kSampleBlack;
         if (pbi < 0 && a.max_depth >= 0) {
-          const double y = (1.0 / __builtin_sqrt(A)) * dy;
+          const double y = (1.0 / sqrt_f64(A)) * dy;  // unit_vector (vec3.h:151-154)
           tt = 0.5 * (y + 1.0);
           kk = (unsigned short)(k < kSampleKCap ? k : kSampleKCap);
         }
@@ -785,8 +805,16 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
           const unsigned s = (unsigned)rc.s_begin + sl;
           rng = splitmix64((((uint64_t)pix) << 32 | (uint64_t)s) ^ rc.seedmix[f]);
           // main.cc:80-81, camera.h:25-28
-          const double u = ((double)i + random_double(rng)) / rc.wm1;
-          const double v = ((double)j + random_double(rng)) / rc.hm1;
+          const double xu = (double)i + random_double(rng);
+          const double xv = (double)j + random_double(rng);
+          double u, v;
+          if (rc.rwm1 != 0.0 && rc.rhm1 != 0.0) {  // uniform: the image is at least 2 x 2
+            u = div_by(xu, rc.wm1, rc.rwm1);
+            v = div_by(xv, rc.hm1, rc.rhm1);
+          } else {
+            u = xu / rc.wm1;
+            v = xv / rc.hm1;
+          }
           const double* cam = rc.cam;  // origin, lower_left, horizontal, vertical
           ox = cam[0], oy = cam[1], oz = cam[2];
           dx = ((cam[3] + u * cam[6]) + v * cam[9]) - ox;
