@@ -43,8 +43,14 @@ constexpr int kTraceWaves = 6;
 // Loop schedule (tuned; re-swept under multi-frame launches in r03,
 // profiles/r03_knobs): compile-time constants, so they take no SGPRs in the
 // loop (held as kernel arguments they pushed SGPRs into VGPR-lane spills).
-constexpr unsigned kRefillMin = 16;  // idle lanes that trigger the finish + refill block
-constexpr unsigned kWalkBatch = 24;  // parked lanes that trigger a batched BVH pass
+#ifndef PSRT_REFILL_MIN
+#define PSRT_REFILL_MIN 16
+#endif
+#ifndef PSRT_WALK_BATCH
+#define PSRT_WALK_BATCH 24
+#endif
+constexpr unsigned kRefillMin = PSRT_REFILL_MIN;  // idle lanes that trigger the finish + refill block
+constexpr unsigned kWalkBatch = PSRT_WALK_BATCH;  // parked lanes that trigger a batched BVH pass
 constexpr unsigned kWalkTail = 4;    // a BVH pass stops once this few lanes still walk
 constexpr int kRngFill = 2;          // look-ahead trials per lane per iteration (min)
 constexpr int kRngExtra = 1;         // extra trials while a scattering lane has none queued
