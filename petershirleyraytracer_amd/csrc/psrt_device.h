@@ -85,4 +85,22 @@ __device__ __forceinline__ bool in_unit_sphere_raw(uint32_t x, uint32_t y, uint3
   return !((wx * wx + wy * wy) + wz * wz > 0x1p62);
 }
 
+// The same test, decided in FP32 except within 2^-20 (relative) of the
+// boundary: f = (float)w (RN, relative error <= 2^-24), S32 = fma(fx, fx,
+// fma(fy, fy, fz*fz)) is within 2^-21 of S = wx^2 + wy^2 + wz^2 (all terms
+// >= 0), and the reference's FP64 sum within 2^-51 of S. So S32 < 2^62
+// (1 - 2^-20) puts the FP64 sum below 2^62 (inside) and S32 > 2^62
+// (1 + 2^-20) above it (outside); the rest (~1.5e-6 of the trials) take the
+// FP64 test, behind a wave-uniform branch.
+__device__ __forceinline__ bool in_unit_sphere_raw_f32(uint32_t x, uint32_t y, uint32_t z) {
+  const float fx = (float)pm1_int_raw(x), fy = (float)pm1_int_raw(y), fz = (float)pm1_int_raw(z);
+  const float s = __builtin_fmaf(fx, fx, __builtin_fmaf(fy, fy, fz * fz));
+  bool in = s < 0x1p62f * (1.0f - 0x1p-20f);
+  const bool undecided = !in && !(s > 0x1p62f * (1.0f + 0x1p-20f));
+  if (__builtin_expect(__ballot(undecided) != 0, 0)) {
+    if (undecided) in = in_unit_sphere_raw(x, y, z);
+  }
+  return in;
+}
+
 }  // namespace psrt

@@ -964,7 +964,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
         uint32_t z, y, x;
         uint64_t nxt;
         raw32_x3(rng, z, y, x, nxt);  // z, y, x: g++'s draw order (vec3.h:78-81); raw outputs
-        const bool in = in_unit_sphere_raw(x, y, z);
+        const bool in = in_unit_sphere_raw_f32(x, y, z);  // FP64 only near the surface
         rng = go ? nxt : rng;
         const bool push = go && in;
         const bool to0 = push && !qv0, to1 = push && qv0;
