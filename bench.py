@@ -25,9 +25,13 @@ The BASELINE's 8-GPU configuration (C4, 3840x2160x500) is
 
 Each timed step ends with the frame's write_color bytes in pinned host memory
 (a device-to-host copy of the rank-0 frame, main.cc:70,86: the reference's
-loop ends by emitting the image). After the timed steps, N > 1 renders one
-untimed frame, gathers its FP64 accumulators to rank 0 and compares sampled
-rows bit for bit with the reference itself (oracle/_ref/ref_render).
+loop ends by emitting the image). After the timed steps the timed kernel's own
+output is checked: its frame of seed --seed against the reference itself
+(oracle/_ref/ref_render) bit for bit on sampled pixels at the frame's full spp
+(N = 1: the CPU baseline's rows, or a column window when spp > 100; N > 1: the
+FP64 accumulators gathered to rank 0, every rank's rows covered), and the last
+frame of the last timed launch against a one-frame render of its seed
+(`batch_check`).
 
 Default workload (BASELINE.json north star, configs[2]): the final
 random-spheres scene (485 spheres), 1200x800, 100 spp, depth 50.
@@ -152,12 +156,14 @@ def host_cpus():
                 cpu_model=model)
 
 
-def run_reference_rows(O, cfg, args, spp, row0, stride, rows, procs, td, tag=""):
+def run_reference_rows(O, cfg, args, spp, row0, stride, rows, procs, td, tag="", col_range=None):
     """oracle/_ref/ref_render on `rows` rows (row0, row0 + stride, ...) at `spp`,
-    columns split over `procs` single-thread processes. Returns (wall seconds,
-    [(c0, c1, accum[rows, c1 - c0, 3])]) or None on failure."""
+    columns (all, or col_range = (c0, c1)) split over `procs` single-thread
+    processes. Returns (wall seconds, [(c0, c1, accum[rows, c1 - c0, 3])]) or
+    None on failure."""
     w, h = cfg["width"], cfg["height"]
-    cols = np.linspace(0, w, procs + 1).astype(int)
+    lo, hi = col_range if col_range else (0, w)
+    cols = np.linspace(lo, hi, procs + 1).astype(int)
     cmds = []
     for p in range(procs):
         if cols[p + 1] <= cols[p]:
@@ -247,29 +253,48 @@ def cpu_baseline(cfg, args, frame_acc):
     return cb, parity
 
 
-def verify_gathered(cfg, args, frame_acc, world):
-    """N > 1: compare sampled rows of the gathered FP64 frame with the
-    reference (every rank's rows are covered: the row stride is odd, so the
-    sampled rows run through every residue mod world)."""
+def reference_parity(cfg, args, frame_acc, world, budget_s=6.0):
+    """Sampled pixels of a full frame's FP64 accumulators compared bit for bit
+    with the reference itself (oracle/_ref/ref_render) at the frame's full spp:
+    whole rows when they fit the budget (~budget_s of CPU on every usable
+    core), else a column window of at least `world` rows (C4 at 500 spp, C5 at
+    10000). The row stride is odd, so the sampled rows run through every
+    residue mod world: every rank's rows are covered."""
     import oracle as O  # checker only
     if not O.have_ref():
         return dict(checked=False, reason="oracle/_ref/ref_render absent")
     w, h, spp = cfg["width"], cfg["height"], cfg["spp"]
-    if frame_acc.shape[0] != h or spp > 100:
-        return dict(checked=False, reason="weak-scaled or >100 spp frame")
+    if frame_acc.shape[0] != h:
+        return dict(checked=False, reason="weak-scaled frame (not the configured one)")
     procs = host_cpus()["usable"]
     rate = 0.62e6 if cfg["scene"] == "two" else 0.0232e6
-    rows = max(world, min(h, int(6.0 * procs * rate / (w * spp))))
+    px = max(1, int(budget_s * procs * rate / spp))  # pixels at full spp within the budget
+    if px >= world * w:  # whole rows
+        rows, cols = max(world, min(h, px // w)), (0, w)
+    else:  # a centred column window over max(world, 8) rows
+        rows = max(world, min(h, 8))
+        nc = max(1, min(w, px // rows))
+        c0 = (w - nc) // 2
+        cols = (c0, c0 + nc)
     stride = max(1, h // rows) | 1
     rows = len(range(0, h, stride))
     with tempfile.TemporaryDirectory() as td:
-        r = run_reference_rows(O, cfg, args, spp, 0, stride, rows, procs, td)
+        r = run_reference_rows(O, cfg, args, spp, 0, stride, rows, min(procs, cols[1] - cols[0]), td,
+                               col_range=cols)
     if r is None:
         return dict(checked=False, reason="reference run failed")
     out = compare_rows(O, r[1], frame_acc, 0, stride, rows, spp)
-    out.update(checked=True, rows=f"0::{stride} ({rows} rows)",
-               ranks_covered=len({(k * stride) % world for k in range(rows)}),
-               gather="RCCL FP64 accumulators" if dist_backend() == "nccl" else dist_backend())
+    out.update(checked=True, rows=f"0::{stride} ({rows} rows)", cols=f"{cols[0]}:{cols[1]}",
+               spp=spp, reference_wall_s=round(r[0], 2),
+               ranks_covered=len({(k * stride) % world for k in range(rows)}))
+    return out
+
+
+def verify_gathered(cfg, args, frame_acc, world):
+    """N > 1: the gathered FP64 frame (a timed frame) against the reference."""
+    out = reference_parity(cfg, args, frame_acc, world)
+    if out.get("checked"):
+        out["gather"] = "RCCL FP64 accumulators" if dist_backend() == "nccl" else dist_backend()
     return out
 
 
@@ -478,6 +503,8 @@ def main():
             return
         is_timed, ev, nb = pending[sl]
         st = ctxs[sl].sync_stats()
+        if is_timed:
+            run["last"] = (sl, nb)  # where the last timed launch's frames are
         if ev is not None:
             ev.synchronize()
         pending[sl] = None
@@ -558,6 +585,14 @@ def main():
     elapsed = timed(depth, args.warmup, args.steps, B, tail_prio)
     kernel_ms = sum(run["kms"]) / sum(run["frames"])  # device time of the trace per frame
     rays = sum(run["rays"]) / sum(run["frames"])      # reference rays per frame
+    # The timed kernel's own output, kept for the checks after the timed
+    # region: the last timed launch's first frame (seed --seed) is the frame
+    # compared with the reference (N = 1: the CPU baseline's pixels; N > 1:
+    # gathered to rank 0), and its last frame (seed --seed + nb - 1) is
+    # compared with a one-frame render of that seed.
+    last_sl, last_nb = run["last"]
+    timed_first = acc[last_sl][0].clone()
+    timed_last = acc[last_sl][last_nb - 1].clone()
     # The same frames one per launch (the unbatched rate, for comparison), and
     # the kernel time for the roofline from one-frame launches one at a time
     # when frames were in flight (their HIP events then span the other frames).
@@ -581,9 +616,38 @@ def main():
     # supplies them; the work is deterministic.
     timed(1, 0, 1, 1, count=True)
     executed = run["exec"]
+    # the batch check: the timed launch's last frame against a one-frame
+    # render of its seed, and its first frame against the counting frame
+    # (seed --seed, one frame per launch, the counting kernel variant)
+    import hashlib
+    torch.cuda.synchronize(dev)
+    counted_first = acc[0][0].clone()
+    prm_last = P.params(w, h, spp, args.max_depth, args.seed + last_nb - 1, off, stride, flags)
+    ctxs[0].render_device_frames(prm_last, 1, [acc[0][0].data_ptr()], None, streams[0].cuda_stream)
+    ctxs[0].sync_stats()
+    torch.cuda.synchronize(dev)
+
+    def sha(t):
+        return hashlib.sha256(t.cpu().numpy().tobytes()).hexdigest()
+    batch_check = {
+        "frames_in_last_timed_launch": last_nb,
+        "last_frame_seed": args.seed + last_nb - 1,
+        "last_frame_sha256_timed": sha(timed_last),
+        "last_frame_sha256_one_frame_launch": sha(acc[0][0]),
+        "first_frame_equal_counting_kernel": bool(torch.equal(timed_first.view(torch.int64),
+                                                              counted_first.view(torch.int64))),
+    }
+    batch_check["last_frame_equal"] = (batch_check["last_frame_sha256_timed"]
+                                       == batch_check["last_frame_sha256_one_frame_launch"])
+    if world > 1:  # the ranks' checks agree on rank 0 only if all pass
+        t = torch.tensor([int(batch_check["last_frame_equal"]
+                              and batch_check["first_frame_equal_counting_kernel"])],
+                         dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        batch_check["all_ranks_equal"] = bool(t.item())
     if world == 1:
-        frame = acc[0][0]  # seed --seed (the counting frame above)
-        rgb = host_rgb[0][0]
+        frame = timed_first  # seed --seed, rendered by the timed kernel
+        rgb = host_rgb[last_sl][0]
 
     # an emulated shard processed only its own rows
     total_samples = (rows if args.emulate_shard else h) * w * spp * args.steps
@@ -601,15 +665,12 @@ def main():
         per_rank = [dict(rank=int(p[0]), rows=int(p[1]), kernel_ms=round(float(p[2]), 3),
                          hbm_frac=round(float(p[3]), 6)) for p in (q.cpu() for q in parts)]
 
-    # N > 1 self-check: one untimed frame, its FP64 accumulators gathered to
-    # rank 0 over the same backend (RCCL), sampled rows compared bit for bit
-    # with the reference itself
+    # N > 1 self-check: the timed kernel's frame of seed --seed, its FP64
+    # accumulators gathered to rank 0 over the same backend (RCCL), sampled
+    # pixels compared bit for bit with the reference itself
     gathered = None
     if world > 1:
-        ctxs[0].render_device(prm, acc[0][0].data_ptr(), 0, streams[0].cuda_stream)
-        ctxs[0].sync_stats()
-        torch.cuda.synchronize(dev)
-        gathered = gather_frame(acc[0][0], h, rank, world)
+        gathered = gather_frame(timed_first, h, rank, world)
         torch.cuda.synchronize(dev)
 
     if rank == 0:
@@ -708,12 +769,20 @@ def main():
         }
         if args.save_ppm and rgb is not None:
             P.write_ppm(args.save_ppm, rgb.cpu().numpy(), binary=True)
+        out["batch_check"] = batch_check
         cb, parity = None, None
         if world == 1 and not args.no_cpu_baseline:
             try:
                 cb, parity = cpu_baseline(cfg, args, frame.cpu().numpy())
             except Exception as e:  # baseline is reported, never the target
                 print(f"cpu baseline failed: {e}", file=sys.stderr)
+            if parity is None and not args.emulate_shard:
+                # spp > 100 (C4, C5): the baseline's rate sample runs at 100 spp,
+                # so the timed frame is checked at its full spp on a column window
+                try:
+                    parity = reference_parity(cfg, args, frame.cpu().numpy(), 1)
+                except Exception as e:  # reported, never the target
+                    parity = dict(checked=False, reason=f"{type(e).__name__}: {e}")
         if world > 1:
             try:
                 parity = verify_gathered(cfg, args, gathered.cpu().numpy(), world)

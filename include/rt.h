@@ -242,7 +242,9 @@ typedef struct {
 typedef struct {
   rt_camera base;     /* origin, lower_left, horizontal, vertical (focus plane) */
   double u[3], v[3];  /* unit lens axes (camera right / up)                     */
-  double lens_radius; /* aperture / 2 (0: a pinhole, no lens draws)             */
+  double lens_radius; /* aperture / 2; the disk is always sampled (the book's
+                         stream), radius 0 only zeroes the offset, so an
+                         aperture-0 camera draws differently from rt_render */
 } rt_camera_lens;
 
 /* camera(lookfrom, lookat, vup, vfov, aspect, aperture, focus_dist) of the
@@ -320,6 +322,13 @@ int rt_debug_world_hit(const rt_sphere* spheres, int n_spheres, const double* ra
  * the record is the reference's whatever the hint. */
 int rt_debug_world_hit_hint(const rt_sphere* spheres, int n_spheres, const double* rays,
                             const int* hints, int count, double* out, int cull);
+
+/* Debug (fault injection, tests only): the context's NEXT render fails with
+ * RT_E_HIP after sample chunk `chunk`'s trace launch and before its reduce, as
+ * a HIP error there would; the hook then clears itself. chunk < 0 clears it.
+ * The failure-recovery path (queue heads and counter sets re-zeroed by the
+ * next render) is tested through it. */
+int rt_debug_fail_after_trace(rt_context* ctx, int chunk);
 
 #ifdef __cplusplus
 }

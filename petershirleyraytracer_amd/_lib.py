@@ -21,7 +21,7 @@ EXPORTS = [
     "rt_camera_default", "rt_camera_look_at", "rt_scene_two_spheres", "rt_scene_random_spheres",
     "rt_scene_parse", "rt_scene_load", "rt_scene_format",
     "rt_last_error", "rt_abi_version", "rt_device_count", "rt_build_info", "rt_debug_probe_f64",
-    "rt_debug_world_hit", "rt_debug_world_hit_hint",
+    "rt_debug_world_hit", "rt_debug_world_hit_hint", "rt_debug_fail_after_trace",
     "rt_camera_look_at_lens", "rt_scene_book_final", "rt_context_set_materials",
     "rt_render_materials",
 ]
@@ -125,6 +125,7 @@ def load(build_if_missing: bool = False):
                                 C.c_int], C.c_int),
         "rt_debug_world_hit_hint": ([P(RtSphere), C.c_int, P(C.c_double), P(C.c_int), C.c_int,
                                      P(C.c_double), C.c_int], C.c_int),
+        "rt_debug_fail_after_trace": ([C.c_void_p, C.c_int], C.c_int),
         "rt_camera_look_at_lens": ([P(C.c_double), P(C.c_double), P(C.c_double), C.c_double,
                                     C.c_double, C.c_double, C.c_double, P(RtCameraLens)],
                                    C.c_int),

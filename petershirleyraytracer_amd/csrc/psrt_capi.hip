@@ -165,6 +165,9 @@ struct rt_context {
   size_t path_cap = 0;    // ints
   rt_stats last{};
   int n_last = 0;
+  bool last_mat = false;  // the last render used RT_FLAG_MATERIALS (no stamps to read)
+  bool failed = false;    // the last render failed part-way (its timings are not reported)
+  int fail_after = -1;    // rt_debug_fail_after_trace: the next render fails after this chunk
 };
 
 namespace {
@@ -605,6 +608,8 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     c->in_flight = true;
     c->last_stream = st;
     c->ev_used = 0;
+    c->failed = false;
+    c->last_mat = mat;
     c->last = rt_stats{};
     c->n_last = c->n;
     return RT_OK;
@@ -621,12 +626,47 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
   // The buffer is sized to the HBM actually free: hipMemGetInfo's free bytes
   // plus this context's current buffer (it is replaced), less a reserve for
   // the GPU's other users, capped by PSRT_SAMPLE_BUF_MB.
+  // The render's other buffers are decided first, so their growth comes out
+  // of the same free HBM: the accumulator scratch (frames without a caller
+  // accumulator, when the frame takes several chunks), the material path
+  // scratch and the camera-ray lists.
+  const bool use_bvh = c->bvh && !(p->flags & RT_FLAG_NO_CULL);
+  // material kernel: the BVH staged in LDS when the workgroups resident per CU
+  // stay as many as without (PSRT_MAT_LDS=0/1 forces it off / on)
+  int mat_grid = use_bvh ? c->grid_mat_bvh : c->grid_mat;
+  unsigned mat_lds = 0;
+  if (mat && use_bvh) {
+    const unsigned bytes = psrt::mat_lds_layout(c->n, c->n_nodes, c->n_leaf, c->n_big).bytes;
+    int pc = 0;
+    const char* ml = std::getenv("PSRT_MAT_LDS");
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, psrt::psrt_trace_mat<true, true, false>,
+                                                     psrt::kMatBlock, bytes) == hipSuccess &&
+        pc >= 1 && (ml ? std::atoi(ml) != 0 : c->cus * pc >= c->grid_mat_bvh)) {
+      mat_lds = bytes;
+      mat_grid = c->cus * pc;
+    }
+  }
+  const size_t mat_lanes = (size_t)mat_grid * psrt::kMatBlock;
+  const size_t path_ints = mat ? mat_lanes * (size_t)std::max(1, p->max_depth) : 0;
+  // camera-ray candidate lists: BVH scenes whose indices fit uint16 and whose
+  // camera lies inside the range the pad covers (|o|_inf <= r_check)
+  const double om = std::max(std::fabs(c->cam.origin[0]),
+                             std::max(std::fabs(c->cam.origin[1]), std::fabs(c->cam.origin[2])));
+  const bool camlist = !mat && use_bvh && c->n < (int)psrt::kCamOverflow && om <= c->r_check &&
+                       !std::getenv("PSRT_NO_CAMLIST");
+  bool any_null_acc = false;
+  for (size_t f = 0; f < nf; ++f) any_null_acc = any_null_acc || !(d_accum_f && d_accum_f[f]);
+  auto grow = [](size_t need, size_t have, size_t unit) { return need > have ? (need - have) * unit : 0; };
+  const size_t other_bytes = (any_null_acc ? grow(nf * P * 3, c->accum_tmp_cap, sizeof(double)) : 0) +
+                             grow(path_ints, c->path_cap, sizeof(int)) +
+                             (camlist ? grow(P, c->plist_cap, sizeof(uint4)) : 0);
   size_t cap_bytes = sample_buffer_cap_bytes();
   {
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
       const size_t usable = fr + c->samples_cap * sizeof(double);
-      cap_bytes = std::min(cap_bytes, usable > kHbmReserve ? usable - kHbmReserve : 0);
+      const size_t keep = kHbmReserve + other_bytes;
+      cap_bytes = std::min(cap_bytes, usable > keep ? usable - keep : 0);
     }
   }
   auto plan = [&](size_t s_max) {
@@ -678,26 +718,10 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
   }
   rc = ensure_events(c, nchunks);
   if (rc) return rc;
-  const bool use_bvh = c->bvh && !(p->flags & RT_FLAG_NO_CULL);
   psrt::MatArgs ma{};
-  // material kernel: the BVH staged in LDS when the workgroups resident per CU
-  // stay as many as without (PSRT_MAT_LDS=0/1 forces it off / on)
-  int mat_grid = use_bvh ? c->grid_mat_bvh : c->grid_mat;
-  unsigned mat_lds = 0;
-  if (mat && use_bvh) {
-    const unsigned bytes = psrt::mat_lds_layout(c->n, c->n_nodes, c->n_leaf, c->n_big).bytes;
-    int pc = 0;
-    const char* ml = std::getenv("PSRT_MAT_LDS");
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, psrt::psrt_trace_mat<true, true, false>,
-                                                     psrt::kMatBlock, bytes) == hipSuccess &&
-        pc >= 1 && (ml ? std::atoi(ml) != 0 : c->cus * pc >= c->grid_mat_bvh)) {
-      mat_lds = bytes;
-      mat_grid = c->cus * pc;
-    }
-  }
   if (mat) {  // the path scratch: one column per resident lane, max_depth rows
-    const size_t lanes = (size_t)mat_grid * psrt::kMatBlock;
-    const size_t need_ints = lanes * (size_t)std::max(1, p->max_depth);
+    const size_t lanes = mat_lanes;
+    const size_t need_ints = path_ints;
     if (c->path_cap < need_ints) {
       rc = quiesce(c);
       if (rc) return rc;
@@ -800,12 +824,6 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
   }
   psrt::BvhView bv = bvh_view(c);
   bv.fixpoint = !(p->flags & RT_FLAG_NO_FIXPOINT) && !std::getenv("PSRT_NO_FIXPOINT");
-  // camera-ray candidate lists: BVH scenes whose indices fit uint16 and whose
-  // camera lies inside the range the pad covers (|o|_inf <= r_check)
-  const double om = std::max(std::fabs(c->cam.origin[0]),
-                             std::max(std::fabs(c->cam.origin[1]), std::fabs(c->cam.origin[2])));
-  const bool camlist = !mat && use_bvh && c->n < (int)psrt::kCamOverflow && om <= c->r_check &&
-                       !std::getenv("PSRT_NO_CAMLIST");
   if (camlist && c->plist_cap < P) {
     rc = quiesce(c);
     if (rc) return rc;
@@ -858,10 +876,10 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
   // marked dirty, the enqueued part is fenced by ev_all1 like a whole render,
   // and the next render re-zeroes them with a stream-ordered memset first.
   c->dirty = true;
-  // test hook (tests/test_gpu_context.py): fail after chunk k's trace launch
-  // and before its reduce, as a HIP error there would
-  const char* fa = std::getenv("PSRT_FAIL_AFTER_TRACE");
-  const int fail_at = fa ? std::atoi(fa) : -1;
+  // fault injection (rt_debug_fail_after_trace, tests only): fail after chunk
+  // k's trace launch and before its reduce, as a HIP error there would; one shot
+  const int fail_at = c->fail_after;
+  c->fail_after = -1;
   auto enqueue_chunks = [&]() -> int {
   for (int ch = 0; ch < nchunks; ++ch) {
     const int s0 = (int)(ch * s_chunk);
@@ -951,7 +969,7 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[2 * ch + 1], st));
     if (ch == fail_at)
-      return set_error(RT_E_HIP, "PSRT_FAIL_AFTER_TRACE: failure injected after chunk %d", ch);
+      return set_error(RT_E_HIP, "rt_debug_fail_after_trace: failure injected after chunk %d", ch);
     // one psrt_reduce per frame; frame 0's also folds the launch's counter
     // sets into the render's totals and re-zeroes the queue heads
     for (size_t f = 0; f < nf; ++f) {
@@ -981,10 +999,19 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
   const hipError_t fence = hipEventRecord(c->ev_all1, st);
   c->in_flight = fence == hipSuccess;
   c->last_stream = st;
-  if (rc) return rc;
+  c->last_mat = mat;
+  if (rc) {
+    // a failed render's timings are not reported: no event pair is summed
+    // (kernel_ms and total_ms read 0 until the next successful render)
+    c->ev_used = 0;
+    c->failed = true;
+    c->last = rt_stats{};
+    return rc;
+  }
   if (fence != hipSuccess)
     return set_error(RT_E_HIP, "hipEventRecord: %s", hipGetErrorString(fence));
   c->dirty = false;
+  c->failed = false;
   c->ev_used = nchunks;
   c->last = rt_stats{};
   c->last.samples = (uint64_t)nf * P * p->spp;
@@ -1002,6 +1029,11 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   }
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipEventSynchronize(c->ev_all1));
+  if (c->failed) {  // waited for the enqueued part; a failed render reports nothing
+    c->last = rt_stats{};
+    if (s) *s = c->last;
+    return RT_OK;
+  }
   // the render's last psrt_reduce wrote its totals into pinned host memory
   unsigned long long cnt[4];
   for (int k = 0; k < 4; ++k) cnt[k] = ((volatile unsigned long long*)c->h_stats)[k];
@@ -1021,7 +1053,7 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   c->last.rays_traced = cnt[3];
   c->last.kernel_ms = kms;
   c->last.total_ms = all;
-  if (std::getenv("PSRT_STAMPS")) {
+  if (std::getenv("PSRT_STAMPS") && !c->last_mat) {
     unsigned long long sec[60];
     HIP_TRY(hipMemcpy(sec, c->d_counters + 8, sizeof sec, hipMemcpyDeviceToHost));
     static const char* names[24] = {"refill", "store", "hit", "hint", "nb", "cam",
@@ -1237,6 +1269,12 @@ int rt_render_materials(const rt_sphere* sph, const rt_material* mats, int n,
 }
 
 // Debug entry: run one f64 primitive on the device (numerics parity tests).
+int rt_debug_fail_after_trace(rt_context* c, int chunk) {
+  if (!c) return set_error(RT_E_INVALID, "rt_debug_fail_after_trace: ctx is NULL");
+  c->fail_after = chunk < 0 ? -1 : chunk;
+  return RT_OK;
+}
+
 int rt_debug_probe_f64(int op, const double* x, const double* y, double* out, int n) {
   if (!x || !y || !out || n < 0) return set_error(RT_E_INVALID, "rt_debug_probe_f64: bad arguments");
   if (n == 0) return RT_OK;

@@ -441,10 +441,16 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
         // and metal lanes share this one loop. (A look-ahead of trials generated
         // a loop iteration ahead, as psrt_trace keeps, was measured 11% slower
         // here: DESIGN.md §14.)
+        // The acceptance test is decided in FP32 with an exact 2^-20 margin,
+        // FP64 only near the surface (psrt_device.h in_unit_sphere_raw_f32).
         uint32_t rz, ry, rx;
         for (;;) {
           raw32_x3(rng, rz, ry, rx, rng);
+#ifdef PSRT_MAT_TRIAL_F64  // A/B build: the FP64 test on every trial
           if (in_unit_sphere_raw(rx, ry, rz)) break;
+#else
+          if (in_unit_sphere_raw_f32(rx, ry, rz)) break;
+#endif
         }
         // random(-1, 1) of each draw, exact from the raw value (psrt_device.h)
         const double x = pm1_raw(rx), y = pm1_raw(ry), z = pm1_raw(rz);

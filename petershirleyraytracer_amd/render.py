@@ -331,6 +331,11 @@ class Context:
                                               arr(d_rgb8), stream or None),
               "rt_render_device_frames")
 
+    def debug_fail_after_trace(self, chunk: int) -> None:
+        """Fault injection (tests only): the next render fails after sample
+        chunk `chunk`'s trace launch, before its reduce (rt_debug_fail_after_trace)."""
+        check(self._L.rt_debug_fail_after_trace(self.handle, chunk), "rt_debug_fail_after_trace")
+
     def stream(self) -> int:
         """The context's own hipStream_t (as an int), used for stream=0."""
         return self._L.rt_context_stream(self.handle) or 0

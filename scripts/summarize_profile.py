@@ -83,13 +83,31 @@ if os.path.exists(trace):
     avg["dispatch_ns"] = d
 fetch = c.get("FETCH_SIZE", 0.0) * 1024 * 2
 write = c.get("WRITE_SIZE", 0.0) * 1024
-secs = avg.get("average_ns_unpipelined", avg.get("average_ns", 0)) * 1e-9
+# The counters are per PMC dispatch (one-frame launches: the PMC passes run
+# bench.py --steps 1), so rates divide by those dispatches' own durations
+# (Start/End_Timestamp of the counter rows, ns), not by the kernel-trace
+# run's average, whose multi-frame dispatches are 20x longer.
+pmc_ns = {}
+for r in rows:
+    if is_timed(r["Kernel_Name"]):
+        a, b = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        pmc_ns[(r["Counter_Name"], a, b)] = b - a
+durs = {}
+for (name, _, _), ns in pmc_ns.items():
+    durs.setdefault(name, []).append(ns)
+pmc_secs = {k: sum(v) / len(v) * 1e-9 for k, v in durs.items()}
+t_all = [ns for v in durs.values() for ns in v]
+secs = sum(t_all) / len(t_all) * 1e-9 if t_all else 0.0
+t_fetch, t_write = pmc_secs.get("FETCH_SIZE", secs), pmc_secs.get("WRITE_SIZE", secs)
+t_grbm = pmc_secs.get("GRBM_GUI_ACTIVE", secs)
 out = {
     "kernel": TIMED, "config": cfg, "kernel_stats": avg, "pmc_dispatches": dispatches,
+    "pmc_dispatch_ms": round(secs * 1e3, 4),
     "hbm_bytes_per_launch": fetch + write,
     "fetch_bytes_per_launch_x2": fetch, "write_bytes_per_launch": write,
-    "hbm_gbps": (fetch + write) / secs / 1e9 if secs else None,
-    "clock_ghz": c["GRBM_GUI_ACTIVE"] / 8 / secs / 1e9 if secs and "GRBM_GUI_ACTIVE" in c else None,
+    "hbm_gbps": (fetch / t_fetch + write / t_write) / 1e9 if t_fetch and t_write else None,
+    "clock_ghz": c["GRBM_GUI_ACTIVE"] / 8 / t_grbm / 1e9 if t_grbm and "GRBM_GUI_ACTIVE" in c else None,
+    "rate_note": "hbm_gbps / clock_ghz: per PMC dispatch, over that pass's own dispatch durations",
     "counters": c,
 }
 if "SQ_INSTS_VALU" in c and "SQ_WAVES" in c:

@@ -46,6 +46,11 @@ def test_bench_single_gpu_line():
     assert "D2H" in d["timed_step"]
     assert d["one_time_ms"]["set_scene"] >= 0 and d["one_time_ms"]["camera_lists"] >= 0
     assert len(d["per_rank"]) == 1
+    # the timed launch's frames: the last against a one-frame render of its seed,
+    # the first against the counting kernel's frame of the same seed
+    bc = d["batch_check"]
+    assert bc["last_frame_equal"] is True and bc["first_frame_equal_counting_kernel"] is True, bc
+    assert bc["frames_in_last_timed_launch"] == d["frames_per_launch"] == 3
     if _have_ref():
         cb = d["cpu_baseline"]
         assert cb["kind"] == "reference" and cb["cores"] >= 1 and cb["one_thread_value"] > 0
@@ -71,3 +76,28 @@ def test_bench_two_ranks_gathered_frame_matches_reference():
         return
     assert par["checked"] is True, par
     assert par["fp64_bit_identical"] is True and par["ranks_covered"] == 2, par
+
+
+def test_bench_two_ranks_c4_gathered_frame_checked():
+    """The BASELINE's 8-GPU configuration (C4, 3840x2160x500), rehearsed at
+    N = 2 over gloo: the gathered timed frame is checked against the
+    reference at its full 500 spp on a column window covering both ranks'
+    rows, and the timed launch's frames against one-frame renders."""
+    env = dict(os.environ, PSRT_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1",
+               OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+           "--gpus", "2", "--config", "c4", "--steps", "1", "--warmup", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=280, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["config_id"] == "c4"
+    assert d["batch_check"]["last_frame_equal"] is True, d["batch_check"]
+    assert d["batch_check"]["all_ranks_equal"] is True, d["batch_check"]
+    par = d["parity_vs_cpu"]
+    if not _have_ref():
+        assert par["checked"] is False
+        return
+    assert par["checked"] is True, par
+    assert par["fp64_bit_identical"] is True and par["ranks_covered"] == 2, par
+    assert par["spp"] == 500, par

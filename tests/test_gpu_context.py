@@ -208,7 +208,7 @@ def test_multi_frame_launch_equals_single_frames(monkeypatch, buf_mb):
 @pytest.mark.parametrize("fail_at", ["0", "1"])
 def test_render_after_a_failure_mid_render(oracle_mod, monkeypatch, fail_at):
     """A render that fails after a trace launch and before its reduce (the
-    PSRT_FAIL_AFTER_TRACE hook stands in for a HIP error there) leaves the
+    rt_debug_fail_after_trace hook stands in for a HIP error there) leaves the
     queue heads and counter sets non-zero: the context is marked dirty, and
     the next render re-zeroes them first and is bit-exact with exact counts.
     fail_at 1: the second of three sample chunks (1 MB sample buffer)."""
@@ -220,11 +220,13 @@ def test_render_after_a_failure_mid_render(oracle_mod, monkeypatch, fail_at):
     ctx = P.Context(0)
     ctx.set_scene(sph, cam)
     acc = torch.zeros((h, w, 3), dtype=torch.float64, device="cuda:0")
-    monkeypatch.setenv("PSRT_FAIL_AFTER_TRACE", fail_at)
+    ctx.debug_fail_after_trace(int(fail_at))
     with pytest.raises(RuntimeError):
         ctx.render_device(P.params(w, h, spp, 50, 3), acc.data_ptr())
-    ctx.sync_stats()  # waits for the part that was enqueued
-    monkeypatch.delenv("PSRT_FAIL_AFTER_TRACE")
+    failed = ctx.sync_stats()  # waits for the part that was enqueued
+    # a failed render reports nothing (no stale timings or counts)
+    assert failed["kernel_ms"] == 0.0 and failed["total_ms"] == 0.0 and failed["rays"] == 0
+    # the hook is one-shot: this render runs in full
     ctx.render_device(P.params(w, h, spp, 50, 3), acc.data_ptr())
     st = ctx.sync_stats()
     want, _, rays = oracle_mod.render(sph, cam, w, h, spp, 50, 3, threads=8)
