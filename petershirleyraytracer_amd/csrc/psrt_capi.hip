@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -118,6 +119,7 @@ struct rt_context {
   hipStream_t stream = nullptr;
   double4* d_geo = nullptr;
   double* d_inv_r = nullptr;
+  float4* d_geo32 = nullptr;  // the FP32 pre-reject's spheres (psrt_kernels.h BvhView::geo32)
   int n = -1;
   int n_cap = 0;
   rt_camera cam{};
@@ -315,6 +317,7 @@ int rt_context_destroy(rt_context* c) {
   if (c->h_stats) (void)hipHostFree(c->h_stats);
   (void)hipFree(c->d_geo);
   (void)hipFree(c->d_inv_r);
+  (void)hipFree(c->d_geo32);
   (void)hipFree(c->d_samples);
   (void)hipFree(c->d_accum_tmp);
   (void)hipFree(c->d_plist);
@@ -341,6 +344,21 @@ int rt_context_destroy(rt_context* c) {
   return RT_OK;
 }
 
+// The FP32 pre-reject's sphere (psrt_kernels.hip test_sphere, Pre32): the
+// centre rounded to nearest and R = |r| + 2^-18 (|c|inf + |r|) + 2^-100
+// rounded up to FP32; +inf (never rejected) beyond 2^40 or for non-finite input.
+static float4 pre32_sphere(const rt_sphere& s) {
+  const double ar = std::fabs(s.r);
+  const double cm = std::max(std::fabs(s.cx), std::max(std::fabs(s.cy), std::fabs(s.cz)));
+  float R = std::numeric_limits<float>::infinity();
+  if (cm + ar <= 0x1p40) {  // false for NaN / inf
+    const double Rd = ar * (1.0 + 0x1p-18) + 0x1p-18 * cm + 0x1p-100;
+    R = (float)Rd;
+    if ((double)R < Rd) R = std::nextafter(R, std::numeric_limits<float>::infinity());
+  }
+  return make_float4((float)s.cx, (float)s.cy, (float)s.cz, R);
+}
+
 int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_camera* cam) {
   if (!c || !cam || n < 0 || (n > 0 && !sph))
     return set_error(RT_E_INVALID, "rt_context_set_scene: bad arguments");
@@ -364,11 +382,14 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
   if (cap > c->n_cap) {
     (void)hipFree(c->d_geo);
     (void)hipFree(c->d_inv_r);
+    (void)hipFree(c->d_geo32);
     c->d_geo = nullptr;
     c->d_inv_r = nullptr;
+    c->d_geo32 = nullptr;
     c->n_cap = 0;
     HIP_TRY(hipMalloc(&c->d_geo, cap * sizeof(double4)));
     HIP_TRY(hipMalloc(&c->d_inv_r, cap * sizeof(double)));
+    HIP_TRY(hipMalloc(&c->d_geo32, cap * sizeof(float4)));
     c->n_cap = cap;
   }
   // uploads on the context's (non-blocking) stream; synchronised below
@@ -379,13 +400,16 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
   // product/quotient the reference forms per call.
   std::vector<double4> geo(cap);
   std::vector<double> inv(cap);
+  std::vector<float4> g32(cap);
   for (int k = 0; k < n; ++k) {
     geo[k] = make_double4(sph[k].cx, sph[k].cy, sph[k].cz, sph[k].r * sph[k].r);
     inv[k] = 1 / sph[k].r;
+    g32[k] = pre32_sphere(sph[k]);
   }
   if (n > 0) {
     HIP_TRY(up(c->d_geo, geo.data(), n * sizeof(double4)));
     HIP_TRY(up(c->d_inv_r, inv.data(), n * sizeof(double)));
+    HIP_TRY(up(c->d_geo32, g32.data(), n * sizeof(float4)));
   }
   c->n = n;
   c->cam = *cam;
@@ -466,6 +490,7 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
 
 static psrt::BvhView bvh_view(const rt_context* c) {
   psrt::BvhView v{};
+  v.geo32 = c->d_geo32;
   v.nodes = c->d_nodes;
   v.leaf_geo = c->d_leaf_geo;
   v.leaf_idx = c->d_leaf_idx;

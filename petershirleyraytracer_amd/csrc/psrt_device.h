@@ -71,8 +71,13 @@ __device__ __forceinline__ int pm1_int_raw(uint32_t raw) {
 __device__ __forceinline__ double w_raw(uint32_t raw) {
   return __hiloint2double(0x43300000, (int)(raw & 0xFFFFFFFEu)) - 0x1.000008p52;
 }
+// pm1 = (m - 2^31) 2^-31 in one FP64 add: the bits {hi 0x41400000, lo m} are
+// the double 2^21 + m 2^-31 (exact: m < 2^32 needs 31 fraction bits below
+// 2^0, the format has 52 below 2^21), and (2^21 + m 2^-31) - (2^21 + 1) =
+// m 2^-31 - 1 is exact (Sterbenz: the operands are within a factor of 2), +0
+// when m = 2^31, as (double)pm1_int_raw(raw) * 2^-31 gives.
 __device__ __forceinline__ double pm1_raw(uint32_t raw) {
-  return w_raw(raw) * 0x1p-31;
+  return __hiloint2double(0x41400000, (int)(raw & 0xFFFFFFFEu)) - 0x1.000008p21;
 }
 
 // random_in_unit_sphere's test !((x*x + y*y) + z*z > 1) (vec3.h:88) on

@@ -34,7 +34,7 @@ constexpr int kShardStride = 16;       // u64 words between heads / counter sets
 // many workgroups per CU stay resident as without (C3: 573 nodes, 485
 // spheres, 41.6 KB; three workgroups).
 struct LdsLayout {
-  unsigned nodes, geo, inv, leaf, nb, bytes;
+  unsigned nodes, geo, inv, leaf, nb, g32, bytes;
 };
 __host__ __device__ inline LdsLayout lds_layout(int n, int n_nodes, int n_leaf) {
   auto a16 = [](unsigned x) { return (x + 15u) & ~15u; };
@@ -44,7 +44,8 @@ __host__ __device__ inline LdsLayout lds_layout(int n, int n_nodes, int n_leaf) 
   l.inv = l.geo + 32u * (unsigned)n;
   l.leaf = a16(l.inv + 8u * (unsigned)n);
   l.nb = a16(l.leaf + 4u * (unsigned)n_leaf);
-  l.bytes = a16(l.nb + 8u * (unsigned)n);  // nb: BvhView::nb_rec
+  l.g32 = a16(l.nb + 8u * (unsigned)n);  // nb: BvhView::nb_rec
+  l.bytes = a16(l.g32 + 16u * (unsigned)n);  // g32: BvhView::geo32
   return l;
 }
 
@@ -133,6 +134,10 @@ struct BvhView {
   // reads one record per query instead of an offset pair and the items
   const uint4* __restrict__ cell_rec;  // [2 * ncell]
   const uint2* __restrict__ nb_rec;    // [n]
+  // per sphere {fl(cx), fl(cy), fl(cz), R}, R >= |r| + 2^-18 (|c|inf + |r|) +
+  // 2^-100 rounded up (+inf beyond 2^40): the FP32 pre-reject (psrt_kernels.hip
+  // Pre32) of test_sphere
+  const float4* __restrict__ geo32;    // [n]
 };
 
 constexpr int kCamTile = 8;         // camera-list tiles are 8 x 8 pixels (one wave)

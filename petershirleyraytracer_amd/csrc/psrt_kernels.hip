@@ -52,8 +52,14 @@ constexpr int kTraceWaves = 6;
 constexpr unsigned kRefillMin = PSRT_REFILL_MIN;  // idle lanes that trigger the finish + refill block
 constexpr unsigned kWalkBatch = PSRT_WALK_BATCH;  // parked lanes that trigger a batched BVH pass
 constexpr unsigned kWalkTail = 4;    // a BVH pass stops once this few lanes still walk
-constexpr int kRngFill = 2;          // look-ahead trials per lane per iteration (min)
-constexpr int kRngExtra = 1;         // extra trials while a scattering lane has none queued
+#ifndef PSRT_RNG_FILL
+#define PSRT_RNG_FILL 2
+#endif
+#ifndef PSRT_RNG_EXTRA
+#define PSRT_RNG_EXTRA 1
+#endif
+constexpr int kRngFill = PSRT_RNG_FILL;    // look-ahead trials per lane per iteration (min)
+constexpr int kRngExtra = PSRT_RNG_EXTRA;  // extra trials while a scattering lane has none queued
 
 __device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
 
@@ -273,32 +279,58 @@ __device__ __forceinline__ int sweep_linear(const double4* __restrict__ geo, int
 // slab error and the FP64 root error; rays it cannot bound (non-finite,
 // |o| > r_check, A not in (0, 1e200)) take the linear sweep.
 
-// sphere.cc:6-31 for one sphere, then the (t, index) rule of the list scan.
-// Pre-reject (exact): when best_t is finite and the origin lies outside the
-// sphere, every point of the sphere is at least
-// D = |amc| - r = C / (|amc| + r) >= C / sqrt(2 (C + 2 r^2)) away, so any root
-// has t*|d| >= D. The computed root's spatial error is <= ~2^-25 |amc| (worst
-// case: tangency, where the discriminant's rounding error is ~2^-52 HALF_B^2).
-// If best_t^2 A * 2 (C + 2 r^2) * (1 + 2^-4) < C^2, every root lies beyond
-// best_t by >= 2^-5 D; that gap exceeds the root error whenever
-// D >= 2^-17 |amc|, guaranteed by C^2 >= 2^-33 (C + r^2)(C + 2 r^2). Origins
-// nearer the surface always take the full test.
+// sphere.cc:6-31 for one sphere, then the (t, index) rule of the list scan,
+// after an exact pre-reject in FP32 (Pre32; r04, replacing r01-r03's FP64
+// one). When the origin lies outside the sphere by D = |amc| - |r|, every
+// root has t |d| >= D; the computed roots are within ~2^-25 |amc| of that
+// (worst case: tangency, where the discriminant's rounding error is ~2^-52
+// HALF_B^2). With o, c and A in range (below), let a = fl(fl(o) - fl(c)) per
+// axis, L = fl(ax^2 + ay^2 + az^2) (two FMAs) and T = fl(fl(bt) sk +
+// fl(mo + R)), where sk >= sqrt(A) (1 + 2^-17), mo >= 2^-18 |o|inf and
+// R >= |r| + 2^-18 (|c|inf + |r|) + 2^-100 (host, rounded up). Rounding
+// analysis (u = 2^-24): |a - amc| <= 3.5u (|o|inf + |c|inf), L <= |a|^2
+// (1 + 3.01u), fl(T T) >= T^2 (1 - u), so L > fl(T T) gives
+// D > bt sqrt(A) (1 + 2^-18.1) + 2^-18.1 (|o|inf + |c|inf + |r|) >= bt sqrt(A)
+// + 2^-20 |amc|: the computed roots exceed bt and the reference rejects them
+// too. Out of range (|o|inf > 2^40, A outside [2^-100, 2^100], |c| or r
+// beyond 2^40, bt = inf or beyond FP32) T, or T^2, is +inf or NaN and nothing
+// is rejected. 10 VALU instructions, mostly FP32, where the FP64 form took
+// ~20 FP64 ones (4 cycles each); its margin (2^-18 relative) rejects at the
+// distances the FP64 one did (D >= 2^-17 |amc|). C3 psrt_trace 12.08 ->
+// 11.80 ms (profiles/r04_pre32/ab.txt); tests/host/pre32_check.c checks it
+// against the reference test on 4 M adversarial cases.
 // Returns false when the pre-reject decided the sphere, true when the full
 // test ran. *c_out (if given) receives C = amc.amc - r^2 as sphere.cc:11 forms it.
+struct Pre32 {
+  float ox, oy, oz;  // fl(o)
+  float sk;          // sqrt(fl(A)) (1 + 2^-16), or +inf: no pre-reject
+  float mo;          // 2^-18 |o|inf (1 + 2^-20)
+};
+
+__device__ __forceinline__ Pre32 pre32_of(double ox, double oy, double oz, double A, double am) {
+  Pre32 p;
+  p.ox = (float)ox, p.oy = (float)oy, p.oz = (float)oz;
+  const bool ok = am <= 0x1p40 && A >= 0x1p-100 && A <= 0x1p100;
+  p.sk = ok ? __builtin_amdgcn_sqrtf((float)A) * (1.0f + 0x1p-16f) : __builtin_inff();
+  p.mo = (float)am * (0x1p-18f * (1.0f + 0x1p-20f));
+  return p;
+}
 
 template <bool kPre = true>
 __device__ __forceinline__ bool test_sphere(const double4 s, int idx, double ox, double oy,
                                             double oz, double dx, double dy, double dz,
                                             double A, double& best_t, int& best_i,
+                                            const float4 s32, const Pre32& pr,
                                             double* c_out = nullptr) {
+  if (kPre) {
+    const float ax = pr.ox - s32.x, ay = pr.oy - s32.y, az = pr.oz - s32.z;
+    const float L = __builtin_fmaf(ax, ax, __builtin_fmaf(ay, ay, az * az));
+    const float T = __builtin_fmaf((float)best_t, pr.sk, pr.mo + s32.w);
+    if (L > T * T) return false;
+  }
   const double ax = ox - s.x, ay = oy - s.y, az = oz - s.z;
   const double c = ((ax * ax + ay * ay) + az * az) - s.w;
   if (c_out) *c_out = c;
-  if (kPre && c > 0.0 && best_t < 1e100) {
-    const double c2 = c * c, k2 = 2.0 * (c + 2.0 * s.w);
-    if (c2 >= 0x1p-34 * (c + s.w) * k2 && (best_t * best_t) * A * k2 * (1.0 + 0x1p-4) < c2)
-      return false;
-  }
   const double hb = (dx * ax + dy * ay) + dz * az;
   const double disc = hb * hb - A * c;
   if (disc < 0.0) return true;
@@ -363,7 +395,8 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
                                           double oz, double dx, double dy, double dz, double A,
                                           double& bt, int& bi, CS& cs, Clock& clk,
                                           bool& trapped, unsigned q,
-                                          const uint2* __restrict__ lnb, const GridC& gc) {
+                                          const uint2* __restrict__ lnb, const GridC& gc,
+                                          const float4* __restrict__ lg32) {
   bt = __builtin_inf();
   bi = -1;
   trapped = false;
@@ -375,6 +408,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     bi = sweep_linear(geo, n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), bt);
     return true;
   }
+  const Pre32 pr = pre32_of(ox, oy, oz, A, am);
   bool fix = false, full = false, nb = false;
   // The candidate list as an inline record {count | i0 << 16, i1 | i2 << 16,
   // ...} (uint16 slots, count kListOverflow = none): a camera ray's pixel list
@@ -387,7 +421,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     const double4 sh = lgeo[hint];
     double ch;
     // the ray's first test: bt = +inf, so no pre-reject
-    test_sphere<false>(sh, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, &ch);
+    test_sphere<false>(sh, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, float4{}, pr, &ch);
     fix = bv.fixpoint && ch == 0.0 && sh.w >= 0x1p-700 && sh.w <= 0x1p700 && am <= 0x1p40;
     ++cs.spheres;
     if (bi == hint) {
@@ -410,7 +444,8 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
   clk.mark(kSecQHint);
   for (int b = 0; b < bv.n_big; ++b) {
     const int idx = bv.big_idx[b];
-    if (idx != hint) full |= test_sphere(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
+    if (idx != hint)
+      full |= test_sphere(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi, bv.geo32[idx], pr);
   }
   cs.spheres += bv.n_big;
   clk.mark(kSecQBig);
@@ -456,7 +491,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     hi >>= 16;
     const int idx = (int)(lo & 0xFFFFu);
     if (idx == hint) continue;
-    full |= test_sphere(lgeo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
+    full |= test_sphere(lgeo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi, lg32[idx], pr);
   }
   cs.spheres += cnt;
   clk.mark(kSecQGrid);
@@ -485,7 +520,8 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
 template <bool kDiag, bool kLdsLeaves, class CS>
 __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __restrict__ nodes,
                                              const int* __restrict__ leaf_idx,
-                                             const double4* __restrict__ lgeo, int hint,
+                                             const double4* __restrict__ lgeo,
+                                             const float4* __restrict__ lg32, int hint,
                                              double ox, double oy, double oz, double dx, double dy,
                                              double dz, double A, double& bt, int& bi,
                                              CS& cs, int& node, unsigned tail) {
@@ -555,11 +591,12 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
         ++cs.leaf_visits;
         if (first_active_lane()) ++cs.wave_leaf_trips;
       }
+      const Pre32 pr = pre32_of(ox, oy, oz, A, am);
       for (int k = first; k < first + cnt; ++k) {
         const int idx = leaf_idx[k];
         if (idx == hint) continue;
         test_sphere(kLdsLeaves ? lgeo[idx] : bv.leaf_geo[k], idx, ox, oy, oz, dx, dy, dz, A, bt,
-                    bi);
+                    bi, lg32[idx], pr);
         ++cs.spheres;
       }
       tmax = tmax_up(bt - t0);
@@ -579,11 +616,11 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
   SectionClock<false> noclk;
   const GridC gc = grid_consts(bv);
   if (!hit_quick(geo, geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs, noclk, trapped,
-                 0u, bv.nb_rec, gc))
+                 0u, bv.nb_rec, gc, bv.geo32))
   {
     int node = 0;
-    hit_traverse<false, false>(bv, bv.nodes, bv.leaf_idx, geo, hint, ox, oy, oz, dx, dy, dz, A,
-                               bt, bi, cs, node, 0u);
+    hit_traverse<false, false>(bv, bv.nodes, bv.leaf_idx, geo, bv.geo32, hint, ox, oy, oz, dx,
+                               dy, dz, A, bt, bi, cs, node, 0u);
   }
   best_t = bt;
   return bi;
@@ -627,6 +664,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
   double* const s_inv = (double*)(s_dyn + lay.inv);
   int* const s_leaf = (int*)(s_dyn + lay.leaf);
   uint2* const s_nb = (uint2*)(s_dyn + lay.nb);
+  float4* const s_g32 = (float4*)(s_dyn + lay.g32);
   // Constants only the refill block reads (camera basis, image size, the
   // divisions' magic numbers, the seed) live in LDS and are re-read on every
   // refill through an offset the compiler cannot see through: held across
@@ -665,7 +703,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
     for (int e = threadIdx.x; e < 2 * (bv.n_nodes + 1); e += blockDim.x) s_nodes[e] = bv.nodes[e];
     for (int e = threadIdx.x; e < a.n; e += blockDim.x) s_geo[e] = geo[e], s_inv[e] = inv_r[e];
     for (int e = threadIdx.x; e < bv.n_leaf; e += blockDim.x) s_leaf[e] = bv.leaf_idx[e];
-    for (int e = threadIdx.x; e < a.n; e += blockDim.x) s_nb[e] = bv.nb_rec[e];
+    for (int e = threadIdx.x; e < a.n; e += blockDim.x) s_nb[e] = bv.nb_rec[e], s_g32[e] = bv.geo32[e];
   }
   __syncthreads();
   const float4* __restrict__ nodes = kLds ? s_nodes : bv.nodes;
@@ -673,6 +711,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
   const double* __restrict__ linv = kLds ? s_inv : inv_r;
   const int* __restrict__ lleaf = kLds ? s_leaf : bv.leaf_idx;
   const uint2* __restrict__ lnb = kLds ? s_nb : bv.nb_rec;
+  const float4* __restrict__ lg32 = kLds ? s_g32 : bv.geo32;
 
   // wave-uniform work window
   uint64_t win_base = 0;
@@ -879,7 +918,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
           asm volatile("" : "+v"(zg));  // re-read the grid constants from LDS here
           const GridC& gc = *(const GridC*)((const char*)&s_gc + zg);
           resolved = hit_quick(geo, lgeo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi,
-                               cs, clk, trapped, q, lnb, gc);
+                               cs, clk, trapped, q, lnb, gc, lg32);
           pending = !resolved;
           wnode = 0;
           if constexpr (kStamps) {
@@ -918,7 +957,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
         __builtin_amdgcn_s_setprio(kWalkPrio);
         if (pending) {
           clk.util(kUWalk);
-          hit_traverse<kStamps, kLds>(bv, nodes, lleaf, lgeo, hint, ox, oy,
+          hit_traverse<kStamps, kLds>(bv, nodes, lleaf, lgeo, lg32, hint, ox, oy,
                                                          oz, dx, dy, dz, A, pbt, pbi, cs, wnode,
                                                          movable ? kWalkTail : 0u);
           if (wnode >= bv.n_nodes) {

@@ -38,6 +38,13 @@ namespace {
 
 constexpr double kTmin = 0.001;
   // the book's world.hit(r, 0.001, infinity)
+// Wave issue priorities (as psrt_trace): the latency-bound
+// sections (the grid query and list tests, the batched walk) issue first,
+// the dependency-light scatter fills the gaps. Book scene: 2.58 -> 2.49 ms
+// per frame (r04, profiles/r04_mat/ab.txt); two BVH nodes per walk trip
+// were slower here (2.72 ms) and are not used.
+constexpr int kMatHitPrio = 2;
+constexpr int kMatWalkPrio = 3;
 
 __device__ __forceinline__ unsigned div_fast(unsigned n, const FastDiv& f) {
   const unsigned t = __umulhi(f.m, n);
@@ -365,8 +372,10 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
         unsigned zg = 0;
         asm volatile("" : "+v"(zg));  // re-read the grid constants from LDS here
         const GridC& gc = *(const GridC*)((const char*)&s_gc + zg);
+        __builtin_amdgcn_s_setprio(kMatHitPrio);
         decided = hit_quick_m<kBVH>(ntests, lgeo, a.n, bv, big_idx, gc, ox, oy, oz, dx, dy, dz,
                                     A, pbt, pbi);
+        __builtin_amdgcn_s_setprio(0);
         pending = !decided;
       }
     }
@@ -374,12 +383,14 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
       const uint64_t pend = __ballot(pending);
       if (pend != 0 && ((unsigned)__popcll(pend) >= a.batch ||
                         __ballot(active && !pending && !fin) == 0)) {
+        __builtin_amdgcn_s_setprio(kMatWalkPrio);
         if (pending) {
           hit_walk_m(ntests, nboxes, bv, nodes, leaf_geo, leaf_idx, ox, oy, oz, dx, dy, dz, A,
                      pbt, pbi);
           pending = false;
           decided = true;
         }
+        __builtin_amdgcn_s_setprio(0);
       }
     }
     if (decided) {
@@ -441,15 +452,17 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
         // and metal lanes share this one loop. (A look-ahead of trials generated
         // a loop iteration ahead, as psrt_trace keeps, was measured 11% slower
         // here: DESIGN.md §14.)
-        // The acceptance test is decided in FP32 with an exact 2^-20 margin,
-        // FP64 only near the surface (psrt_device.h in_unit_sphere_raw_f32).
+        // The acceptance test stays in FP64 here: psrt_trace's FP32
+        // pre-decision (psrt_device.h in_unit_sphere_raw_f32) was 1.5% slower
+        // in this divergent loop (its ballot runs per trial; r04,
+        // profiles/r04_mat/ab.txt).
         uint32_t rz, ry, rx;
         for (;;) {
           raw32_x3(rng, rz, ry, rx, rng);
-#ifdef PSRT_MAT_TRIAL_F64  // A/B build: the FP64 test on every trial
-          if (in_unit_sphere_raw(rx, ry, rz)) break;
-#else
+#ifdef PSRT_MAT_TRIAL_F32  // A/B build
           if (in_unit_sphere_raw_f32(rx, ry, rz)) break;
+#else
+          if (in_unit_sphere_raw(rx, ry, rz)) break;
 #endif
         }
         // random(-1, 1) of each draw, exact from the raw value (psrt_device.h)
