@@ -686,7 +686,13 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
                              grow(path_ints, c->path_cap, sizeof(int)) +
                              (camlist ? grow(P, c->plist_cap, sizeof(uint4)) : 0);
   size_t cap_bytes = sample_buffer_cap_bytes();
-  {
+  // the current buffer already holds the whole render in one chunk: no query
+  // (hipMemGetInfo is a host round trip on every render otherwise)
+  const size_t recs_all = nf * P * (size_t)p->spp;
+  const size_t need_all = mat ? 3 * recs_all : recs_all + (recs_all + 3) / 4;  // doubles
+  const bool fits = c->d_samples && c->samples_cap >= need_all && (size_t)p->spp <= s_units &&
+                    need_all * sizeof(double) <= cap_bytes && other_bytes == 0;
+  if (!fits) {
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
       const size_t usable = fr + c->samples_cap * sizeof(double);

@@ -63,6 +63,18 @@ constexpr int kRngExtra = PSRT_RNG_EXTRA;  // extra trials while a scattering la
 
 __device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
 
+// Section ablation (measurement builds only, PSRT_ABLATE = section id): the
+// section runs a second time on copies of its state, the copy's results sunk
+// here, so PMC SQ_INSTS_VALU and the kernel time grow by that section's cost
+// (DESIGN.md §4 census). The default build has PSRT_ABLATE = 0.
+#ifndef PSRT_ABLATE
+#define PSRT_ABLATE 0
+#endif
+template <class T>
+__device__ __forceinline__ void ablate_sink(T v) {
+  asm volatile("" ::"v"(v));
+}
+
 // Diagnostic build only (kStamps): wave-level cycle accounting per kernel
 // section, one s_memtime per boundary (cdna_hip_programming.md §7 stamps).
 // Read its SHARES, never its run time.
@@ -91,7 +103,11 @@ struct SectionClock {
   // workgroup's LDS (LDS atomics by the first active lane); flushed at exit
   unsigned* ucnt = nullptr;
   __device__ __forceinline__ void util(int u) {
+#ifdef PSRT_STAMPS_NO_UTIL  // section clocks only: no LDS atomics inside the sections
+    if constexpr (false) {
+#else
     if constexpr (kOn) {
+#endif
       const uint64_t m = __ballot(1);
       if (first_active_lane()) {
         atomicAdd(ucnt + 2 * u, 1u);
@@ -422,6 +438,14 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     double ch;
     // the ray's first test: bt = +inf, so no pre-reject
     test_sphere<false>(sh, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, float4{}, pr, &ch);
+#if PSRT_ABLATE == 6
+    {
+      double bt2 = __builtin_inf(), ch2;
+      int bi2 = -1;
+      test_sphere<false>(sh, hint, ox, oy, oz, dx, dy, dz, A, bt2, bi2, float4{}, pr, &ch2);
+      ablate_sink(bt2), ablate_sink(bi2), ablate_sink(ch2);
+    }
+#endif
     fix = bv.fixpoint && ch == 0.0 && sh.w >= 0x1p-700 && sh.w <= 0x1p700 && am <= 0x1p40;
     ++cs.spheres;
     if (bi == hint) {
@@ -442,6 +466,19 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     }
   }
   clk.mark(kSecQHint);
+#if PSRT_ABLATE == 7
+  {
+    double bt2 = bt;
+    int bi2 = bi;
+    bool f2 = false;
+    for (int b = 0; b < bv.n_big; ++b) {
+      const int idx = bv.big_idx[b];
+      if (idx != hint)
+        f2 |= test_sphere(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt2, bi2, bv.geo32[idx], pr);
+    }
+    ablate_sink(bt2), ablate_sink(bi2), ablate_sink(f2);
+  }
+#endif
   for (int b = 0; b < bv.n_big; ++b) {
     const int idx = bv.big_idx[b];
     if (idx != hint)
@@ -485,6 +522,22 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
   }
   const int cnt = listed ? (int)(rec.x & 0xFFFFu) : 0;
   uint64_t lo = rec.x | (uint64_t)rec.y << 32, hi = rec.z | (uint64_t)rec.w << 32;
+#if PSRT_ABLATE == 8
+  {
+    double bt2 = bt;
+    int bi2 = bi;
+    bool f2 = false;
+    uint64_t lo2 = lo, hi2 = hi;
+    for (int e = 0; e < cnt; ++e) {
+      lo2 = (lo2 >> 16) | (hi2 << 48);
+      hi2 >>= 16;
+      const int idx = (int)(lo2 & 0xFFFFu);
+      if (idx == hint) continue;
+      f2 |= test_sphere(lgeo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt2, bi2, lg32[idx], pr);
+    }
+    ablate_sink(bt2), ablate_sink(bi2), ablate_sink(f2);
+  }
+#endif
   for (int e = 0; e < cnt; ++e) {
     clk.util(kUListTrip);
     lo = (lo >> 16) | (hi << 48);
@@ -848,6 +901,18 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
           const int j = rc.hm1_i - r;
           const unsigned pix = (unsigned)j * dw.d + i;
           const unsigned s = (unsigned)rc.s_begin + sl;
+#if PSRT_ABLATE == 5
+          {
+            uint64_t r2 = splitmix64((((uint64_t)pix) << 32 | (uint64_t)s) ^ rc.seedmix[f]);
+            const double xu2 = (double)i + random_double(r2), xv2 = (double)j + random_double(r2);
+            const double u2 = div_by(xu2, rc.wm1, rc.rwm1), v2 = div_by(xv2, rc.hm1, rc.rhm1);
+            const double* c2 = rc.cam;
+            const double ex = ((c2[3] + u2 * c2[6]) + v2 * c2[9]) - c2[0];
+            const double ey = ((c2[4] + u2 * c2[7]) + v2 * c2[10]) - c2[1];
+            const double ez = ((c2[5] + u2 * c2[8]) + v2 * c2[11]) - c2[2];
+            ablate_sink((ex * ex + ey * ey) + ez * ez), ablate_sink(r2);
+          }
+#endif
           rng = splitmix64((((uint64_t)pix) << 32 | (uint64_t)s) ^ rc.seedmix[f]);
           // main.cc:80-81, camera.h:25-28
           const double xu = (double)i + random_double(rng);
@@ -919,6 +984,17 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
           const GridC& gc = *(const GridC*)((const char*)&s_gc + zg);
           resolved = hit_quick(geo, lgeo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi,
                                cs, clk, trapped, q, lnb, gc, lg32);
+#if PSRT_ABLATE == 1
+          {
+            double bt2;
+            int bi2;
+            bool tr2;
+            CullStatsT<false> cs2{0u, 0u};
+            const bool r2 = hit_quick(geo, lgeo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt2,
+                                      bi2, cs2, clk, tr2, q, lnb, gc, lg32);
+            ablate_sink(bt2), ablate_sink(bi2), ablate_sink(tr2), ablate_sink(r2);
+          }
+#endif
           pending = !resolved;
           wnode = 0;
           if constexpr (kStamps) {
@@ -957,6 +1033,16 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
         __builtin_amdgcn_s_setprio(kWalkPrio);
         if (pending) {
           clk.util(kUWalk);
+#if PSRT_ABLATE == 2
+          {
+            double bt2 = pbt;
+            int bi2 = pbi, n2 = wnode;
+            CullStatsT<false> cs2{0u, 0u};
+            hit_traverse<false, kLds>(bv, nodes, lleaf, lgeo, lg32, hint, ox, oy, oz, dx, dy, dz,
+                                      A, bt2, bi2, cs2, n2, movable ? kWalkTail : 0u);
+            ablate_sink(bt2), ablate_sink(bi2), ablate_sink(n2);
+          }
+#endif
           hit_traverse<kStamps, kLds>(bv, nodes, lleaf, lgeo, lg32, hint, ox, oy,
                                                          oz, dx, dy, dz, A, pbt, pbi, cs, wnode,
                                                          movable ? kWalkTail : 0u);
@@ -992,6 +1078,32 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
     // without a trial then keeps its resolved hit and scatters in a later
     // iteration (sc_wait): its draws stay in stream order either way.
     const bool want = (resolved && !finish) || sc_wait;
+#if PSRT_ABLATE == 3
+    {
+      const bool can_fill = active && !finish;
+      uint64_t rng2 = rng;
+      uint32_t a0x = q0x, a0y = q0y, a0z = q0z, a1x = q1x, a1y = q1y, a1z = q1z;
+      bool v0 = qv0, v1 = qv1;
+      int f = 0;
+      do {
+        const bool go = can_fill && !v1;
+        uint32_t z, y, x;
+        uint64_t nxt;
+        raw32_x3(rng2, z, y, x, nxt);
+        const bool in = in_unit_sphere_raw_f32(x, y, z);
+        rng2 = go ? nxt : rng2;
+        const bool push = go && in;
+        const bool to0 = push && !v0, to1 = push && v0;
+        a0x = to0 ? x : a0x, a0y = to0 ? y : a0y, a0z = to0 ? z : a0z;
+        a1x = to1 ? x : a1x, a1y = to1 ? y : a1y, a1z = to1 ? z : a1z;
+        v1 = v1 || to1;
+        v0 = v0 || to0;
+        ++f;
+      } while (f < kRngFill || (f < kRngFill + kRngExtra && __ballot(want && !v0) != 0));
+      ablate_sink(rng2), ablate_sink(a0x), ablate_sink(a0y), ablate_sink(a0z);
+      ablate_sink(a1x), ablate_sink(a1y), ablate_sink(a1z), ablate_sink(v0), ablate_sink(v1);
+    }
+#endif
     {
       const bool can_fill = active && !finish;
       // branch-free body: every lane computes a trial; only lanes with room
@@ -1021,6 +1133,18 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
     // ---- scatter: target = (p + n) + random_in_hemisphere(n)  (main.cc:42-43) ----
     const bool have = qv0;
     sc_wait = want && !have;
+#if PSRT_ABLATE == 4
+    if (want && have) {
+      const HitRec h = hit_record_of(lgeo[hit], linv[hit], t, ox, oy, oz, dx, dy, dz);
+      double rx = pm1_raw(q0x), ry = pm1_raw(q0y), rz = pm1_raw(q0z);
+      if (!((rx * h.nx + ry * h.ny) + rz * h.nz > 0.0)) rx = -rx, ry = -ry, rz = -rz;
+      const double ex = ((h.px + h.nx) + rx) - h.px;
+      const double ey = ((h.py + h.ny) + ry) - h.py;
+      const double ez = ((h.pz + h.nz) + rz) - h.pz;
+      ablate_sink((ex * ex + ey * ey) + ez * ez), ablate_sink(h.px), ablate_sink(h.py);
+      ablate_sink(h.pz);
+    }
+#endif
     if (want && have) {
       clk.util(kUScatter);
       const HitRec h = hit_record_of(lgeo[hit], linv[hit], t, ox, oy, oz, dx, dy, dz);
