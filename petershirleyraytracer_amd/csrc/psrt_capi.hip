@@ -1001,26 +1001,52 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     HIP_TRY(hipEventRecord(c->ev[2 * ch + 1], st));
     if (ch == fail_at)
       return set_error(RT_E_HIP, "rt_debug_fail_after_trace: failure injected after chunk %d", ch);
-    // one psrt_reduce per frame; frame 0's also folds the launch's counter
-    // sets into the render's totals and re-zeroes the queue heads
-    for (size_t f = 0; f < nf; ++f) {
+    // psrt_reduce: frames whose accumulators and bytes are evenly strided
+    // (the bench's, torch's [B, rows, W, 3] blocks) are reduced by ONE launch
+    // (blockIdx.y = frame: the frames' reduces overlap instead of running back
+    // to back with a launch gap each); other pointer sets by one launch per
+    // frame. Frame 0's block 0 also folds the launch's counter sets into the
+    // render's totals and re-zeroes the queue heads.
+    const bool last = ch == nchunks - 1;
+    auto strided = [&](auto* const* v, size_t& stride) {
+      stride = 0;
+      if (nf == 1) return true;
+      for (size_t f = 0; f < nf; ++f)
+        if ((v[f] == nullptr) != (v[0] == nullptr)) return false;
+      if (!v[0]) return true;
+      const ptrdiff_t d = v[1] - v[0];
+      if (d <= 0) return false;
+      for (size_t f = 1; f < nf; ++f)
+        if (v[f] - v[f - 1] != d) return false;
+      stride = (size_t)d;
+      return true;
+    };
+    size_t acc_stride = 0, rgb_stride = 0;
+    std::vector<unsigned char*> rgb_now(nf, nullptr);
+    for (size_t f = 0; f < nf; ++f) rgb_now[f] = last ? rgb[f] : nullptr;
+    const bool one = strided(acc.data(), acc_stride) && strided(rgb_now.data(), rgb_stride);
+    for (size_t f0 = 0; f0 < nf; f0 += one ? nf : 1) {
       psrt::ReduceArgs ra{};
-      ra.samp_t = c->d_samples + f * fu;
+      ra.samp_t = c->d_samples + f0 * fu;
       // the k array follows the t array of all frames
-      ra.samp_k = (const unsigned short*)(c->d_samples + nf * fu) + f * fu;
+      ra.samp_k = (const unsigned short*)(c->d_samples + nf * fu) + f0 * fu;
       ra.pixels = (unsigned)P;
       ra.s_count = sc;
       ra.first_chunk = ch == 0;
       ra.spp_total = p->spp;
-      ra.accum = acc[f];
-      ra.rgb8 = (ch == nchunks - 1) ? rgb[f] : nullptr;
-      ra.fold_stats = f == 0;
+      ra.accum = acc[f0];
+      ra.rgb8 = rgb_now[f0];
+      ra.frame_units = fu;
+      ra.accum_stride = acc_stride;
+      ra.rgb8_stride = rgb_stride;
+      ra.fold_stats = f0 == 0;
       ra.heads = c->d_counters + kHeads;
       ra.sets = c->d_counters + kSets;
       ra.totals = c->d_counters + kTotals;
-      ra.host_stats = (ch == nchunks - 1 && f == 0) ? c->d_stats : nullptr;
+      ra.host_stats = (last && f0 == 0) ? c->d_stats : nullptr;
       const unsigned blocks = (unsigned)((P + psrt::kReduceBlock - 1) / psrt::kReduceBlock);
-      hipLaunchKernelGGL(psrt::psrt_reduce, dim3(blocks), dim3(psrt::kReduceBlock), 0, st, ra);
+      hipLaunchKernelGGL(psrt::psrt_reduce, dim3(blocks, one ? (unsigned)nf : 1u),
+                         dim3(psrt::kReduceBlock), 0, st, ra);
       HIP_TRY(hipGetLastError());
     }
   }

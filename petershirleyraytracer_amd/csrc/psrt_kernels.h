@@ -165,6 +165,14 @@ struct ReduceArgs {
   double* accum;          // [pixels][3] (required unless single chunk + rgb only)
   unsigned char* rgb8;    // [pixels][3] or nullptr (last chunk only)
   int fold_stats;         // block 0 folds the counter sets (one reduce per launch: frame 0's)
+  // psrt_reduce over the frames of a multi-frame launch in ONE launch (r04):
+  // blockIdx.y = frame f, whose records start f * frame_units into samp_t /
+  // samp_k and whose sums / bytes go to accum + f * accum_stride / rgb8 +
+  // f * rgb8_stride (the caller's frames evenly strided; plain offsets: an
+  // array of pointers in the arguments, indexed by f, put them in scratch)
+  size_t frame_units;
+  size_t accum_stride;  // doubles
+  size_t rgb8_stride;   // bytes
   // Statistics and queue state of the trace launch before this reduce
   // (block 0 only): the counter sets are added into totals (reset on the first
   // chunk), then the sets and the queue heads are zeroed for the next launch;

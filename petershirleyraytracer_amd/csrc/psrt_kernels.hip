@@ -1216,6 +1216,14 @@ PSRT_INSTANTIATE(true, true, true)
 // last chunk (color.h:8-24).
 
 __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
+  if (blockIdx.y > 0) {  // frame blockIdx.y of a multi-frame launch
+    const size_t f = blockIdx.y;
+    a.samp_t += f * a.frame_units;
+    a.samp_k += f * a.frame_units;
+    if (a.accum) a.accum += f * a.accum_stride;
+    if (a.rgb8) a.rgb8 += f * a.rgb8_stride;
+    a.fold_stats = 0;
+  }
   // the trace launch's sharded counter sets -> totals (-> host), then the
   // sets and queue heads back to zero (ReduceArgs; stream order puts this
   // after every trace block and before the context's next launch)
