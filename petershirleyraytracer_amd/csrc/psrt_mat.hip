@@ -46,6 +46,23 @@ constexpr double kTmin = 0.001;
 constexpr int kMatHitPrio = 2;
 constexpr int kMatWalkPrio = 3;
 
+// Section ablation (measurement builds only, PSRT_MAT_ABLATE = section id, as
+// psrt_trace's PSRT_ABLATE): 1 hit_quick_m, 2 the batched walk, 3 the
+// random_in_unit_sphere trial loop, 4 the hit record, 5 the refill's per-lane
+// setup run a second time on laundered copies of their inputs, results sunk.
+#ifndef PSRT_MAT_ABLATE
+#define PSRT_MAT_ABLATE 0
+#endif
+template <class T>
+__device__ __forceinline__ void mat_sink(T v) {
+  asm volatile("" ::"v"(v));
+}
+template <class T>
+__device__ __forceinline__ T mat_launder(T v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 __device__ __forceinline__ unsigned div_fast(unsigned n, const FastDiv& f) {
   const unsigned t = __umulhi(f.m, n);
   return (t + ((n - t) >> f.sh1)) >> f.sh2;
@@ -259,6 +276,47 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
   auto mat_fuzz = [&](int i) { return kLm ? lmat[i].w : a.mats[i].fuzz; };
   auto mat_ir = [&](int i) { return kLm ? lmat[i].w : a.mats[i].ir; };
 
+  // the refill's per-lane setup of unit su_: its stream, main.cc:80-81 and
+  // the thin-lens get_ray (book ch. 12)
+  auto setup = [&](unsigned su_, uint64_t& rng_, double& ox_, double& oy_, double& oz_,
+                   double& dx_, double& dy_, double& dz_, double& A_) {
+    unsigned q = div_fast(su_, a.div_s);  // f * pixels + pixel (frame-major units)
+    const unsigned sl = su_ - q * a.div_s.d;
+    unsigned f = 0;
+    if (a.frames > 1) {
+      f = div_fast(q, a.div_p);
+      q -= f * a.div_p.d;
+    }
+    const unsigned row_k = div_fast(q, a.div_w);
+    const unsigned i = q - row_k * a.div_w.d;
+    const int j = (a.height - 1) - (a.row_offset + (int)row_k * a.row_stride);
+    const unsigned pix = (unsigned)j * (unsigned)a.width + i;
+    const unsigned s = (unsigned)a.s_begin + sl;
+    rng_ = splitmix64((((uint64_t)pix) << 32 | (uint64_t)s) ^ a.seedmix[f]);
+    // main.cc:80-81
+    const double u = ((double)i + random_double(rng_)) / (double)(a.width - 1);
+    const double v = ((double)j + random_double(rng_)) / (double)(a.height - 1);
+    // thin lens (book ch. 12): rd = lens_radius * random_in_unit_disk()
+    // (vec3(random_double(-1,1), random_double(-1,1), 0): draws y, x)
+    double px, py;
+    for (;;) {
+      py = pm1(rng_);
+      px = pm1(rng_);
+      if (!((px * px + py * py) + 0.0 * 0.0 >= 1.0)) break;
+    }
+    const double rx = a.lens_radius * px, ry = a.lens_radius * py;
+    const double fx = a.lu[0] * rx + a.lv[0] * ry;
+    const double fy = a.lu[1] * rx + a.lv[1] * ry;
+    const double fz = a.lu[2] * rx + a.lv[2] * ry;
+    ox_ = a.org[0] + fx;
+    oy_ = a.org[1] + fy;
+    oz_ = a.org[2] + fz;
+    dx_ = (((a.llc[0] + u * a.hor[0]) + v * a.ver[0]) - a.org[0]) - fx;
+    dy_ = (((a.llc[1] + u * a.hor[1]) + v * a.ver[1]) - a.org[1]) - fy;
+    dz_ = (((a.llc[2] + u * a.hor[2]) + v * a.ver[2]) - a.org[2]) - fz;
+    A_ = (dx_ * dx_ + dy_ * dy_) + dz_ * dz_;
+  };
+
   uint64_t win_base = 0;
   unsigned win_left = 0;
   unsigned qnext = 0;  // heads found past the end of the work (this block's first)
@@ -306,41 +364,16 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
         else if (fresh) unit = nb + (rank - win_left);
         if (unit < total) {
           su = (unsigned)unit;
-          unsigned q = div_fast(su, a.div_s);  // f * pixels + pixel (frame-major units)
-          const unsigned sl = su - q * a.div_s.d;
-          unsigned f = 0;
-          if (a.frames > 1) {
-            f = div_fast(q, a.div_p);
-            q -= f * a.div_p.d;
+          setup(su, rng, ox, oy, oz, dx, dy, dz, A);
+#if PSRT_MAT_ABLATE == 5
+          {
+            uint64_t r2;
+            double o2x, o2y, o2z, d2x, d2y, d2z, A2;
+            setup(mat_launder(su), r2, o2x, o2y, o2z, d2x, d2y, d2z, A2);
+            mat_sink(r2), mat_sink(o2x), mat_sink(o2y), mat_sink(o2z), mat_sink(d2x),
+                mat_sink(d2y), mat_sink(d2z), mat_sink(A2);
           }
-          const unsigned row_k = div_fast(q, a.div_w);
-          const unsigned i = q - row_k * a.div_w.d;
-          const int j = (a.height - 1) - (a.row_offset + (int)row_k * a.row_stride);
-          const unsigned pix = (unsigned)j * (unsigned)a.width + i;
-          const unsigned s = (unsigned)a.s_begin + sl;
-          rng = splitmix64((((uint64_t)pix) << 32 | (uint64_t)s) ^ a.seedmix[f]);
-          // main.cc:80-81
-          const double u = ((double)i + random_double(rng)) / (double)(a.width - 1);
-          const double v = ((double)j + random_double(rng)) / (double)(a.height - 1);
-          // thin lens (book ch. 12): rd = lens_radius * random_in_unit_disk()
-          // (vec3(random_double(-1,1), random_double(-1,1), 0): draws y, x)
-          double px, py;
-          for (;;) {
-            py = pm1(rng);
-            px = pm1(rng);
-            if (!((px * px + py * py) + 0.0 * 0.0 >= 1.0)) break;
-          }
-          const double rx = a.lens_radius * px, ry = a.lens_radius * py;
-          const double fx = a.lu[0] * rx + a.lv[0] * ry;
-          const double fy = a.lu[1] * rx + a.lv[1] * ry;
-          const double fz = a.lu[2] * rx + a.lv[2] * ry;
-          ox = a.org[0] + fx;
-          oy = a.org[1] + fy;
-          oz = a.org[2] + fz;
-          dx = (((a.llc[0] + u * a.hor[0]) + v * a.ver[0]) - a.org[0]) - fx;
-          dy = (((a.llc[1] + u * a.hor[1]) + v * a.ver[1]) - a.org[1]) - fy;
-          dz = (((a.llc[2] + u * a.hor[2]) + v * a.ver[2]) - a.org[2]) - fz;
-          A = (dx * dx + dy * dy) + dz * dz;
+#endif
           k = 0;
           np = 0;
           active = true;
@@ -375,6 +408,17 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
         __builtin_amdgcn_s_setprio(kMatHitPrio);
         decided = hit_quick_m<kBVH>(ntests, lgeo, a.n, bv, big_idx, gc, ox, oy, oz, dx, dy, dz,
                                     A, pbt, pbi);
+#if PSRT_MAT_ABLATE == 1
+        {
+          double bt2;
+          int bi2;
+          const bool d2 = hit_quick_m<kBVH>(ntests, lgeo, a.n, bv, big_idx, gc, mat_launder(ox),
+                                            mat_launder(oy), mat_launder(oz), mat_launder(dx),
+                                            mat_launder(dy), mat_launder(dz), mat_launder(A), bt2,
+                                            bi2);
+          mat_sink(bt2), mat_sink(bi2), mat_sink(d2);
+        }
+#endif
         __builtin_amdgcn_s_setprio(0);
         pending = !decided;
       }
@@ -385,8 +429,18 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
                         __ballot(active && !pending && !fin) == 0)) {
         __builtin_amdgcn_s_setprio(kMatWalkPrio);
         if (pending) {
+#if PSRT_MAT_ABLATE == 2
+          double bt2 = mat_launder(pbt);
+          int bi2 = mat_launder(pbi);
+#endif
           hit_walk_m(ntests, nboxes, bv, nodes, leaf_geo, leaf_idx, ox, oy, oz, dx, dy, dz, A,
                      pbt, pbi);
+#if PSRT_MAT_ABLATE == 2
+          hit_walk_m(ntests, nboxes, bv, nodes, leaf_geo, leaf_idx, mat_launder(ox), mat_launder(oy),
+                     mat_launder(oz), mat_launder(dx), mat_launder(dy), mat_launder(dz),
+                     mat_launder(A), bt2, bi2);
+          mat_sink(bt2), mat_sink(bi2);
+#endif
           pending = false;
           decided = true;
         }
@@ -418,6 +472,16 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
     if (resolved) {
       const int bi = pbi;
       const HitRec h = hit_record_of(lgeo[bi], linv[bi], pbt, ox, oy, oz, dx, dy, dz);
+#if PSRT_MAT_ABLATE == 4
+      {
+        const int bi2 = mat_launder(bi);
+        const HitRec h2 = hit_record_of(lgeo[bi2], linv[bi2], mat_launder(pbt), mat_launder(ox),
+                                        mat_launder(oy), mat_launder(oz), mat_launder(dx),
+                                        mat_launder(dy), mat_launder(dz));
+        mat_sink(h2.px), mat_sink(h2.py), mat_sink(h2.pz), mat_sink(h2.nx), mat_sink(h2.ny),
+            mat_sink(h2.nz), mat_sink(h2.front);
+      }
+#endif
       const int kind = mat_kind(bi);
       double ndx = 0.0, ndy = 0.0, ndz = 0.0;
       bool ok = true;
@@ -456,6 +520,17 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
         // pre-decision (psrt_device.h in_unit_sphere_raw_f32) was 1.5% slower
         // in this divergent loop (its ballot runs per trial; r04,
         // profiles/r04_mat/ab.txt).
+#if PSRT_MAT_ABLATE == 3
+        {
+          uint64_t r2 = mat_launder(rng);
+          uint32_t z2, y2, x2;
+          for (;;) {
+            raw32_x3(r2, z2, y2, x2, r2);
+            if (in_unit_sphere_raw(x2, y2, z2)) break;
+          }
+          mat_sink(z2), mat_sink(y2), mat_sink(x2), mat_sink(r2);
+        }
+#endif
         uint32_t rz, ry, rx;
         for (;;) {
           raw32_x3(rng, rz, ry, rx, rng);
