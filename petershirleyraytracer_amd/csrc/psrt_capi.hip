@@ -127,6 +127,13 @@ struct rt_context {
   size_t samples_cap = 0;  // doubles
   double* d_accum_tmp = nullptr;
   size_t accum_tmp_cap = 0;  // doubles
+  // the material integrator's camera-ray lists through the lens
+  // (psrt_mat_camera_lists), cached per (materials / lens camera, W, H,
+  // row_offset, row_stride)
+  uint4* d_mat_plist = nullptr;
+  size_t mat_plist_cap = 0;  // records
+  bool mat_plist_valid = false;
+  int mat_plist_key[4] = {0, 0, 0, 0};
   uint4* d_plist = nullptr;  // camera-ray candidate lists, one uint4 per owned pixel
   size_t plist_cap = 0;      // records
   // The lists depend only on the scene, camera, frame size and shard: they
@@ -134,6 +141,7 @@ struct rt_context {
   bool plist_valid = false;
   int plist_key[4] = {0, 0, 0, 0};
   hipEvent_t ev_plist = nullptr;  // after the lists' build (other streams wait on it)
+  hipEvent_t ev_mat_plist = nullptr;  // the same for the material lists
   unsigned long long* d_wave_log = nullptr;  // diagnostic (PSRT_STAMPS): per-wave timeline
   size_t wave_log_cap = 0, wave_log_used = 0;
   // [8, 128) diagnostic stamps; queue heads at kHeads, statistics counter sets
@@ -306,6 +314,7 @@ int rt_context_create(int device, rt_context** out) {
   HIP_TRY(hipEventCreate(&c->ev_all0));
   HIP_TRY(hipEventCreate(&c->ev_all1));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_plist, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&c->ev_mat_plist, hipEventDisableTiming));
   *out = c;
   return RT_OK;
 }
@@ -321,6 +330,7 @@ int rt_context_destroy(rt_context* c) {
   (void)hipFree(c->d_samples);
   (void)hipFree(c->d_accum_tmp);
   (void)hipFree(c->d_plist);
+  (void)hipFree(c->d_mat_plist);
   (void)hipFree(c->d_wave_log);
   (void)hipFree(c->d_counters);
   (void)hipFree(c->d_nodes);
@@ -339,6 +349,7 @@ int rt_context_destroy(rt_context* c) {
   if (c->ev_all0) (void)hipEventDestroy(c->ev_all0);
   if (c->ev_all1) (void)hipEventDestroy(c->ev_all1);
   if (c->ev_plist) (void)hipEventDestroy(c->ev_plist);
+  if (c->ev_mat_plist) (void)hipEventDestroy(c->ev_mat_plist);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return RT_OK;
@@ -378,6 +389,7 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
   }
   c->scene.clear();  // set again once every structure is built
   c->has_mats = false;  // materials belong to the scene they were set for
+  c->mat_plist_valid = false;
   const int cap = n > 0 ? n : 1;
   if (cap > c->n_cap) {
     (void)hipFree(c->d_geo);
@@ -679,12 +691,20 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
                              std::max(std::fabs(c->cam.origin[1]), std::fabs(c->cam.origin[2])));
   const bool camlist = !mat && use_bvh && c->n < (int)psrt::kCamOverflow && om <= c->r_check &&
                        !std::getenv("PSRT_NO_CAMLIST");
+  // the material integrator's lists through the lens: the same conditions,
+  // for the lens camera's origin
+  const double lom = std::max(std::fabs(c->lcam.base.origin[0]),
+                              std::max(std::fabs(c->lcam.base.origin[1]),
+                                       std::fabs(c->lcam.base.origin[2])));
+  const bool mat_list = mat && use_bvh && c->n < (int)psrt::kCamOverflow && lom <= c->r_check &&
+                        !std::getenv("PSRT_NO_CAMLIST");
   bool any_null_acc = false;
   for (size_t f = 0; f < nf; ++f) any_null_acc = any_null_acc || !(d_accum_f && d_accum_f[f]);
   auto grow = [](size_t need, size_t have, size_t unit) { return need > have ? (need - have) * unit : 0; };
   const size_t other_bytes = (any_null_acc ? grow(nf * P * 3, c->accum_tmp_cap, sizeof(double)) : 0) +
                              grow(path_ints, c->path_cap, sizeof(int)) +
-                             (camlist ? grow(P, c->plist_cap, sizeof(uint4)) : 0);
+                             (camlist ? grow(P, c->plist_cap, sizeof(uint4)) : 0) +
+                             (mat_list ? grow(P, c->mat_plist_cap, sizeof(uint4)) : 0);
   size_t cap_bytes = sample_buffer_cap_bytes();
   // the current buffer already holds the whole render in one chunk: no query
   // (hipMemGetInfo is a host round trip on every render otherwise)
@@ -855,6 +875,16 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
   }
   psrt::BvhView bv = bvh_view(c);
   bv.fixpoint = !(p->flags & RT_FLAG_NO_FIXPOINT) && !std::getenv("PSRT_NO_FIXPOINT");
+  if (mat_list && c->mat_plist_cap < P) {
+    rc = quiesce(c);
+    if (rc) return rc;
+    (void)hipFree(c->d_mat_plist);
+    c->d_mat_plist = nullptr;
+    c->mat_plist_cap = 0;
+    HIP_TRY(hipMalloc(&c->d_mat_plist, P * sizeof(uint4)));
+    c->mat_plist_cap = P;
+    c->mat_plist_valid = false;
+  }
   if (camlist && c->plist_cap < P) {
     rc = quiesce(c);
     if (rc) return rc;
@@ -901,6 +931,37 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     std::copy(key, key + 4, c->plist_key);
     c->plist_valid = true;
     bv.plist = c->d_plist;
+  }
+  if (mat_list && c->mat_plist_valid && std::equal(key, key + 4, c->mat_plist_key)) {
+    HIP_TRY(hipStreamWaitEvent(st, c->ev_mat_plist, 0));
+    ma.plist = c->d_mat_plist;
+  } else if (mat_list) {
+    psrt::MatCamListArgs la{};
+    for (int k = 0; k < 3; ++k) {
+      la.org[k] = c->lcam.base.origin[k];
+      la.llc[k] = c->lcam.base.lower_left[k];
+      la.hor[k] = c->lcam.base.horizontal[k];
+      la.ver[k] = c->lcam.base.vertical[k];
+    }
+    la.lens_radius = std::fabs(c->lcam.lens_radius);
+    la.width = p->width;
+    la.height = p->height;
+    la.row_offset = p->row_offset;
+    la.row_stride = p->row_stride;
+    la.rows = rows;
+    la.leaf_geo = c->d_leaf_geo;
+    la.leaf_idx = c->d_leaf_idx;
+    la.n_leaf = c->n_leaf;
+    la.pad = c->pad;
+    la.plist = c->d_mat_plist;
+    const dim3 lg((p->width + psrt::kCamTile - 1) / psrt::kCamTile,
+                  (rows + psrt::kCamTile - 1) / psrt::kCamTile);
+    hipLaunchKernelGGL(psrt::psrt_mat_camera_lists, lg, dim3(64), 0, st, la);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev_mat_plist, st));
+    std::copy(key, key + 4, c->mat_plist_key);
+    c->mat_plist_valid = true;
+    ma.plist = c->d_mat_plist;
   }
   // A HIP failure after the first trace launch would leave the queue heads and
   // counter sets non-zero (only psrt_reduce re-zeroes them): the context is
@@ -1286,6 +1347,7 @@ int rt_context_set_materials(rt_context* c, const rt_material* mats, int n,
     HIP_TRY(hipStreamSynchronize(c->stream));
   }
   c->lcam = *cam;
+  c->mat_plist_valid = false;
   c->has_mats = true;
   return RT_OK;
 }

@@ -198,7 +198,10 @@ static_assert(sizeof(DevMaterial) == 48, "device material layout");
 #endif
 constexpr int kMatBlock = PSRT_MAT_BLOCK;
 #ifndef PSRT_MAT_WAVES
-#define PSRT_MAT_WAVES 5  // waves per SIMD asked of the register allocator (96 VGPRs)
+// waves per SIMD asked of the register allocator: 4 (up to 128 VGPRs) —
+// LDS already holds the kernel to two 512-thread workgroups (4 waves per
+// SIMD); 5 (96 VGPRs) cost 3% (r04, profiles/r04_matlist)
+#define PSRT_MAT_WAVES 4
 #endif
 constexpr int kMatWaves = PSRT_MAT_WAVES;
 constexpr unsigned kMatChunk = 256;  // units per queue ticket
@@ -226,6 +229,23 @@ struct MatArgs {
   int* __restrict__ path;
   unsigned path_stride;
   unsigned batch;  // parked lanes that trigger a batched BVH walk
+  // per-pixel candidate lists of the camera rays through the lens
+  // (psrt_mat_camera_lists; CamListArgs format), or nullptr
+  const uint4* __restrict__ plist;
+};
+
+// Camera-ray candidate lists for the thin lens (psrt_mat_camera_lists):
+// every ray of pixel (i, j) starts on the lens disk (radius lens_radius about
+// the origin) and passes through the pixel's patch of the focus plane.
+struct MatCamListArgs {
+  double org[3], llc[3], hor[3], ver[3];
+  double lens_radius;
+  int width, height, row_offset, row_stride, rows;
+  const double4* __restrict__ leaf_geo;  // BVH spheres {cx, cy, cz, r*r} per leaf slot
+  const int* __restrict__ leaf_idx;      // original index per leaf slot
+  int n_leaf;
+  double pad;                            // BVH box padding (absolute)
+  uint4* __restrict__ plist;             // [rows * width]
 };
 
 // psrt_trace_mat<true, true> stages the scene in dynamic LDS: BVH nodes (2
@@ -256,6 +276,7 @@ __global__ void psrt_trace_mat(const double4* __restrict__ geo, const double* __
                                double* __restrict__ rgb, MatArgs a, BvhView bv);
 // psrt_reduce over colour records: samp_t holds [pixels][s_count][3] doubles
 __global__ void psrt_reduce_rgb(ReduceArgs a);
+__global__ void psrt_mat_camera_lists(MatCamListArgs a);
 
 template <bool kBVH, bool kStamps, bool kLds, bool kCount>
 __global__ void psrt_trace(const double4* __restrict__ geo, const double* __restrict__ inv_r,

@@ -118,8 +118,8 @@ template <bool kBVH, bool kCount>
 __device__ __forceinline__ bool hit_quick_m(TestCount<kCount>& nt, const double4* __restrict__ geo,
                                             int n, const BvhView& bv,
                                             const int* __restrict__ big_idx, const GridC& gc,
-                                            double ox, double oy, double oz, double dx, double dy,
-                                            double dz, double A, double& bt, int& bi) {
+                                            uint4 rec, double ox, double oy, double oz, double dx,
+                                            double dy, double dz, double A, double& bt, int& bi) {
   bt = __builtin_inf();
   bi = -1;
   const double am = __builtin_fmax(__builtin_fabs(ox),
@@ -135,6 +135,20 @@ __device__ __forceinline__ bool hit_quick_m(TestCount<kCount>& nt, const double4
     test_sphere_m(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
   }
   nt.add((unsigned)bv.n_big);
+  // a camera ray with its pixel's candidate list (psrt_mat_camera_lists): the
+  // listed BVH spheres are every one a ray of the pixel can hit
+  const unsigned ncand = rec.x & 0xFFFFu;
+  if (ncand != kCamOverflow) {
+    uint64_t lo = rec.x | (uint64_t)rec.y << 32, hi = rec.z | (uint64_t)rec.w << 32;
+    for (unsigned e = 0; e < ncand; ++e) {
+      lo = (lo >> 16) | (hi << 48);
+      hi >>= 16;
+      const int idx = (int)(lo & 0xFFFFu);
+      test_sphere_m(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
+    }
+    nt.add(ncand);
+    return true;
+  }
   // FP32 grid query, exact within 256 S (psrt_trace hit_quick)
   const double rg = 4.0 * gc.r_check;
   const int cell = (am <= rg && (bt * bt) * A <= rg * rg)
@@ -279,7 +293,7 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
   // the refill's per-lane setup of unit su_: its stream, main.cc:80-81 and
   // the thin-lens get_ray (book ch. 12)
   auto setup = [&](unsigned su_, uint64_t& rng_, double& ox_, double& oy_, double& oz_,
-                   double& dx_, double& dy_, double& dz_, double& A_) {
+                   double& dx_, double& dy_, double& dz_, double& A_, unsigned& pq_) {
     unsigned q = div_fast(su_, a.div_s);  // f * pixels + pixel (frame-major units)
     const unsigned sl = su_ - q * a.div_s.d;
     unsigned f = 0;
@@ -287,6 +301,7 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
       f = div_fast(q, a.div_p);
       q -= f * a.div_p.d;
     }
+    pq_ = q;
     const unsigned row_k = div_fast(q, a.div_w);
     const unsigned i = q - row_k * a.div_w.d;
     const int j = (a.height - 1) - (a.row_offset + (int)row_k * a.row_stride);
@@ -327,6 +342,7 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
   int k = 0, np = 0;  // hits so far / attenuating hits kept in `path`
   uint64_t rng = 0;   // the sample's stream: position of its next draw
   unsigned su = 0;
+  unsigned pq = 0;    // the sample's pixel within the shard (camera list index)
   unsigned long long rays = 0;
   // Rays the grid cannot decide park (pending) with their partial (pbt, pbi)
   // and are walked together once a.batch lanes wait or nothing else can move
@@ -364,12 +380,14 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
         else if (fresh) unit = nb + (rank - win_left);
         if (unit < total) {
           su = (unsigned)unit;
-          setup(su, rng, ox, oy, oz, dx, dy, dz, A);
+          setup(su, rng, ox, oy, oz, dx, dy, dz, A, pq);
 #if PSRT_MAT_ABLATE == 5
           {
             uint64_t r2;
             double o2x, o2y, o2z, d2x, d2y, d2z, A2;
-            setup(mat_launder(su), r2, o2x, o2y, o2z, d2x, d2y, d2z, A2);
+            unsigned q2;
+            setup(mat_launder(su), r2, o2x, o2y, o2z, d2x, d2y, d2z, A2, q2);
+            mat_sink(q2);
             mat_sink(r2), mat_sink(o2x), mat_sink(o2y), mat_sink(o2z), mat_sink(d2x),
                 mat_sink(d2y), mat_sink(d2z), mat_sink(A2);
           }
@@ -406,13 +424,15 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
         asm volatile("" : "+v"(zg));  // re-read the grid constants from LDS here
         const GridC& gc = *(const GridC*)((const char*)&s_gc + zg);
         __builtin_amdgcn_s_setprio(kMatHitPrio);
-        decided = hit_quick_m<kBVH>(ntests, lgeo, a.n, bv, big_idx, gc, ox, oy, oz, dx, dy, dz,
-                                    A, pbt, pbi);
+        uint4 rec = make_uint4(kCamOverflow, 0u, 0u, 0u);
+        if (k == 0 && a.plist) rec = a.plist[pq];  // camera ray: its pixel's list
+        decided = hit_quick_m<kBVH>(ntests, lgeo, a.n, bv, big_idx, gc, rec, ox, oy, oz, dx, dy,
+                                    dz, A, pbt, pbi);
 #if PSRT_MAT_ABLATE == 1
         {
           double bt2;
           int bi2;
-          const bool d2 = hit_quick_m<kBVH>(ntests, lgeo, a.n, bv, big_idx, gc, mat_launder(ox),
+          const bool d2 = hit_quick_m<kBVH>(ntests, lgeo, a.n, bv, big_idx, gc, rec, mat_launder(ox),
                                             mat_launder(oy), mat_launder(oz), mat_launder(dx),
                                             mat_launder(dy), mat_launder(dz), mat_launder(A), bt2,
                                             bi2);
@@ -655,6 +675,127 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce_rgb(ReduceArgs a) {
       a.rgb8[(size_t)q * 3 + ch] = (unsigned char)(int)(255.999 * x);
     }
   }
+}
+
+// ---- camera-ray candidate lists through the thin lens ----
+//
+// A camera ray of pixel (i, j) starts at x = o + offset, |x - o| <= rho (the
+// lens radius; u, v are unit axes), and passes through a point y of the
+// pixel's patch Q of the focus plane: y = (llc + s h) + t v with s in
+// [i, i+1]/(W-1), t in [j, j+1]/(H-1) (main.cc:80-81). With the patch centre
+// q_c, L = |q_c - o|, the axis a = (q_c - o)/L and r_Q = max |y - q_c| (at a
+// corner: Q is a parallelogram), the ray's point x + u (y - x), u >= 0, lies
+// within |1-u| rho + u r_Q <= rho + u (rho + r_Q) of o + u (q_c - o). So every
+// ray of the pixel lies in the cone of apex o, axis a and half-angle
+// asin((rho + r_Q)/L), dilated by rho; a sphere can return an accepted root
+// only if its padded ball (r + pad, the BVH's root-error pad) dilated by rho
+// meets that cone. The FP64 cone is widened (k by 2^-20 relative, the angle by
+// 1e-9 rad, the ball by 2^-20), margins far above its own rounding. The tile
+// and per-pixel passes follow psrt_camera_lists; rho = 0 is the pinhole.
+
+namespace {
+
+struct LensCone {
+  double ax, ay, az, ca, sa;  // unit axis, cos / sin of the widened half-angle
+  bool ok;
+};
+
+__device__ __forceinline__ void focus_point(const MatCamListArgs& a, double s, double t,
+                                            double q[3]) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) q[k] = (a.llc[k] + s * a.hor[k]) + t * a.ver[k];
+}
+
+__device__ __forceinline__ LensCone lens_cone(const MatCamListArgs& a, double s0, double s1,
+                                              double t0, double t1) {
+  LensCone c;
+  double qc[3];
+  focus_point(a, 0.5 * (s0 + s1), 0.5 * (t0 + t1), qc);
+  const double dx = qc[0] - a.org[0], dy = qc[1] - a.org[1], dz = qc[2] - a.org[2];
+  const double L = __builtin_sqrt((dx * dx + dy * dy) + dz * dz);
+  c.ax = dx / L, c.ay = dy / L, c.az = dz / L;
+  double rq = 0.0;
+  const double ss[2] = {s0, s1}, ts[2] = {t0, t1};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    double y[3];
+    focus_point(a, ss[e & 1], ts[e >> 1], y);
+    const double ex = y[0] - qc[0], ey = y[1] - qc[1], ez = y[2] - qc[2];
+    rq = __builtin_fmax(rq, __builtin_sqrt((ex * ex + ey * ey) + ez * ez));
+  }
+  const double k = (a.lens_radius + rq) / L * (1.0 + 0x1p-20) + 1e-12;
+  c.ca = __builtin_sqrt(__builtin_fmax(0.0, 1.0 - k * k)) - 1e-9;  // cos(asin k), widened
+  c.sa = __builtin_sqrt(__builtin_fmax(0.0, 1.0 - c.ca * c.ca));
+  c.ok = L > 0.0 && L < 1e300 && k < 0.99 && c.ca > 0.1;  // narrow, finite cone (else no lists)
+  return c;
+}
+
+// Does the ball (centre s.xyz, radius sqrt(s.w) + pad + rho) meet the cone?
+__device__ __forceinline__ bool lens_cone_meets(const LensCone& c, const MatCamListArgs& a,
+                                                const double4 s) {
+  const double cx = s.x - a.org[0], cy = s.y - a.org[1], cz = s.z - a.org[2];
+  const double l2 = (cx * cx + cy * cy) + cz * cz;
+  const double R = (__builtin_sqrt(s.w) + a.pad + a.lens_radius) * (1.0 + 0x1p-20);
+  if (!(l2 > R * R * (1.0 + 0x1p-20))) return true;  // apex inside / near the ball (or NaN)
+  const double l = __builtin_sqrt(l2);
+  const double cb = ((c.ax * cx + c.ay * cy) + c.az * cz) / l;
+  if (cb >= c.ca) return true;  // centre inside the cone
+  const double sb = __builtin_sqrt(__builtin_fmax(0.0, 1.0 - cb * cb));
+  // angle(axis, centre) - half-angle must be <= asin(R / l) (<= pi/2)
+  const double cosd = cb * c.ca + sb * c.sa, sind = sb * c.ca - cb * c.sa;
+  return cosd >= 0.0 && sind <= R / l;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(64) void psrt_mat_camera_lists(MatCamListArgs a) {
+  __shared__ int s_tile[kCamTileCap];
+  const unsigned lane = __lane_id();
+  const int x0 = blockIdx.x * kCamTile, r0 = blockIdx.y * kCamTile;
+  const int x1 = min(x0 + kCamTile, a.width), r1 = min(r0 + kCamTile, a.rows);
+  const int px = x0 + (int)(lane % kCamTile), rk = r0 + (int)(lane / kCamTile);
+  const double iw = 1.0 / (double)(a.width - 1), ih = 1.0 / (double)(a.height - 1);
+  // reference rows j = H-1-r fall as the shard row rk rises (main.cc:72)
+  const int jhi = a.height - 1 - (a.row_offset + r0 * a.row_stride);
+  const int jlo = a.height - 1 - (a.row_offset + (r1 - 1) * a.row_stride);
+  // s, t bounds widened by a relative 2^-40 (the rounding of i + random_double()
+  // and of the division)
+  const double wid = 1.0 + 0x1p-40;
+  const LensCone tc = lens_cone(a, x0 * iw / wid, x1 * iw * wid, jlo * ih / wid,
+                                (jhi + 1) * ih * wid);
+  int cnt = 0;
+  bool over = !tc.ok;
+  for (int base = 0; base < a.n_leaf && !over; base += 64) {
+    const int k = base + (int)lane;
+    const bool cand = k < a.n_leaf && lens_cone_meets(tc, a, a.leaf_geo[k]);
+    const uint64_t m = __ballot(cand);
+    const int pos = cnt + (int)lanes_below(m);
+    if (cand && pos < kCamTileCap) s_tile[pos] = k;
+    cnt += __popcll(m);
+    if (cnt > kCamTileCap) over = true;
+  }
+  __syncthreads();
+  if (px >= a.width || rk >= a.rows) return;
+  const int j = a.height - 1 - (a.row_offset + rk * a.row_stride);
+  unsigned w[4] = {kCamOverflow, 0u, 0u, 0u};
+  if (!over) {
+    const LensCone pc = lens_cone(a, px * iw / wid, (px + 1) * iw * wid, j * ih / wid,
+                                  (j + 1) * ih * wid);
+    unsigned n = 0;
+    bool full = !pc.ok;
+    for (int e = 0; e < cnt && !full; ++e) {
+      const int k = s_tile[e];
+      if (!lens_cone_meets(pc, a, a.leaf_geo[k])) continue;
+      if (n == (unsigned)kCamPixelCap) {
+        full = true;
+        break;
+      }
+      ++n;  // slot n of 8 uint16 (slot 0 = count)
+      w[n >> 1] |= (unsigned)a.leaf_idx[k] << ((n & 1) * 16);
+    }
+    if (!full) w[0] = (w[0] & 0xFFFF0000u) | n;
+  }
+  a.plist[(size_t)rk * a.width + px] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 }  // namespace psrt

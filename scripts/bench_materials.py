@@ -81,6 +81,12 @@ def main():
         roof["valu_issue"] = {"simd_cycles_per_valu_inst": round(d.get("simd_cycles_per_valu", 0), 3),
                               "wait_inst_frac": round(d.get("wait_inst_frac", 0), 3),
                               "source": "profiles/pmc_mat.json"}
+        if d.get("hbm_bytes_per_launch"):
+            # FETCH_SIZE x 2 + WRITE_SIZE per one-frame PMC dispatch (KiB-corrected)
+            roof["traffic"] = d["hbm_bytes_per_launch"]
+            roof["traffic_note"] = ("HBM bytes per frame from the PMC passes (profiles/pmc_mat.json); "
+                                    "algorithmic: 24 B colour record per sample written, read once "
+                                    "by psrt_reduce_rgb")
     out = {
         "metric": "Msamples/sec (materials extension, book final scene)",
         "value": W * H * S / (step * 1e3),

@@ -112,6 +112,9 @@ out = {
 }
 if "SQ_INSTS_VALU" in c and "SQ_WAVES" in c:
     out["valu_insts_per_wave"] = c["SQ_INSTS_VALU"] / c["SQ_WAVES"]
+if "SQ_WAIT_INST_ANY" in c and c.get("SQ_WAVE_CYCLES"):
+    # wave cycles spent waiting for an instruction's operands (latency)
+    out["wait_inst_frac"] = c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"]
 if "GRBM_GUI_ACTIVE" in c:
     cyc = c["GRBM_GUI_ACTIVE"] / 8  # one XCD's clock over the launch
     for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_BRANCH"):

@@ -133,12 +133,18 @@ def test_long_paths_between_mirrors(oracle_mod):
 
 
 @pytest.mark.parametrize("aperture", [0.1, 2.0, 0.0])
-def test_apertures_bit_exact(oracle_mod, book, aperture):
-    """The book's aperture, a wide one and a pinhole, at 240 x 160 x 6."""
+def test_apertures_bit_exact(oracle_mod, book, monkeypatch, aperture):
+    """The book's aperture, a wide one and a pinhole, at 240 x 160 x 6.
+    Camera rays through the lens test only their pixel's candidate list
+    (psrt_mat_camera_lists): the frame equals the one without
+    lists (PSRT_NO_CAMLIST) bit for bit, and the oracle's."""
     sp, mt, _ = book
     W, H, spp = 240, 160, 6
     lens = oracle_mod.camera_look_at_lens(aspect=W / H, aperture=aperture)
     acc, rgb, st = P.render_materials(sp, mt, _lens(lens), W, H, spp, 50, 13)
+    monkeypatch.setenv("PSRT_NO_CAMLIST", "1")
+    acc2, _, st2 = P.render_materials(sp, mt, _lens(lens), W, H, spp, 50, 13)
+    assert np.array_equal(bits(acc), bits(acc2)) and st["rays"] == st2["rays"]
     ref, rays = oracle_mod.render_mat(sp, mt, lens, W, H, spp, 50, 13, threads=8)
     assert np.array_equal(bits(acc), bits(ref)) and st["rays"] == rays
     assert np.array_equal(rgb, oracle_mod.quantize(ref, spp))
