@@ -1032,7 +1032,7 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     const dim3 blk(psrt::kTraceBlock);
     // scene data in LDS when three workgroups per CU still fit (the BVH
     // kernel's resident count otherwise: its global-memory variant)
-    const unsigned lds_bytes = psrt::lds_layout(c->n, c->n_nodes, c->n_leaf).bytes;
+    const unsigned lds_bytes = psrt::lds_layout(c->n, c->n_nodes, c->n_leaf, c->n_big).bytes;
     const bool lds = use_bvh && lds_bytes <= c->lds_max && !std::getenv("PSRT_NO_LDS");
     // PSRT_BLOCKS_PER_CU: measurement knob (occupancy sweep), default = resident max
     const char* bpc = std::getenv("PSRT_BLOCKS_PER_CU");

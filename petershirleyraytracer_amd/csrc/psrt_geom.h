@@ -134,6 +134,7 @@ struct GridC {
   float a0[3], a1[3];
   int top[3], pad_;
   double r_check, nb_c2;
+  const uint4* plist;  // BvhView::plist (psrt_trace's camera lists), or nullptr
 };
 
 __device__ __forceinline__ GridC grid_consts(const BvhView& bv) {
@@ -150,6 +151,7 @@ __device__ __forceinline__ GridC grid_consts(const BvhView& bv) {
   g.pad_ = 0;
   g.r_check = bv.r_check;
   g.nb_c2 = bv.nb_c2;
+  g.plist = bv.plist;
   return g;
 }
 

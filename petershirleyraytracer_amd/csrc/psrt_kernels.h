@@ -30,13 +30,14 @@ constexpr int kQueues = PSRT_QUEUES;
 constexpr int kShardStride = 16;       // u64 words between heads / counter sets (128 B)
 // Scene data psrt_trace stages in (dynamic) LDS per workgroup: BVH nodes (2
 // float4 each, plus the padding node), spheres {c, r*r}, 1/r, leaf slots and
-// neighbour records (8 B); byte offsets, 16-B aligned. The host stages them when as
+// neighbour records (8 B), FP32 pre-reject spheres and the big-sphere
+// indices; byte offsets, 16-B aligned. The host stages them when as
 // many workgroups per CU stay resident as without (C3: 573 nodes, 485
 // spheres, 41.6 KB; three workgroups).
 struct LdsLayout {
-  unsigned nodes, geo, inv, leaf, nb, g32, bytes;
+  unsigned nodes, geo, inv, leaf, nb, g32, big, bytes;
 };
-__host__ __device__ inline LdsLayout lds_layout(int n, int n_nodes, int n_leaf) {
+__host__ __device__ inline LdsLayout lds_layout(int n, int n_nodes, int n_leaf, int n_big) {
   auto a16 = [](unsigned x) { return (x + 15u) & ~15u; };
   LdsLayout l;
   l.nodes = 0;
@@ -45,7 +46,8 @@ __host__ __device__ inline LdsLayout lds_layout(int n, int n_nodes, int n_leaf) 
   l.leaf = a16(l.inv + 8u * (unsigned)n);
   l.nb = a16(l.leaf + 4u * (unsigned)n_leaf);
   l.g32 = a16(l.nb + 8u * (unsigned)n);  // nb: BvhView::nb_rec
-  l.bytes = a16(l.g32 + 16u * (unsigned)n);  // g32: BvhView::geo32
+  l.big = a16(l.g32 + 16u * (unsigned)n);  // g32: BvhView::geo32
+  l.bytes = a16(l.big + 4u * (unsigned)(n_big > 0 ? n_big : 1));  // big: BvhView::big_idx
   return l;
 }
 

@@ -412,7 +412,8 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
                                           double& bt, int& bi, CS& cs, Clock& clk,
                                           bool& trapped, unsigned q,
                                           const uint2* __restrict__ lnb, const GridC& gc,
-                                          const float4* __restrict__ lg32) {
+                                          const float4* __restrict__ lg32,
+                                          const int* __restrict__ lbig) {
   bt = __builtin_inf();
   bi = -1;
   trapped = false;
@@ -431,7 +432,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
   // (psrt_camera_lists), loaded early; the hint sphere's neighbour record or
   // the grid list's replace it below.
   uint4 rec = make_uint4(kCamOverflow, 0u, 0u, 0u);
-  if (hint < 0 && bv.plist) rec = bv.plist[q];
+  if (hint < 0 && gc.plist) rec = gc.plist[q];  // from LDS (GridC), not a spilled SGPR pair
   if (hint >= 0) {
     clk.util(kUHint);
     const double4 sh = lgeo[hint];
@@ -472,17 +473,19 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     int bi2 = bi;
     bool f2 = false;
     for (int b = 0; b < bv.n_big; ++b) {
-      const int idx = bv.big_idx[b];
+      const int idx = lbig[b];
       if (idx != hint)
-        f2 |= test_sphere(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt2, bi2, bv.geo32[idx], pr);
+        f2 |= test_sphere(lgeo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt2, bi2, lg32[idx], pr);
     }
     ablate_sink(bt2), ablate_sink(bi2), ablate_sink(f2);
   }
 #endif
+  // the big spheres from the scene copy in LDS (kLds; the global arrays
+  // otherwise): their indices, spheres and FP32 spheres
   for (int b = 0; b < bv.n_big; ++b) {
-    const int idx = bv.big_idx[b];
+    const int idx = lbig[b];
     if (idx != hint)
-      full |= test_sphere(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi, bv.geo32[idx], pr);
+      full |= test_sphere(lgeo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi, lg32[idx], pr);
   }
   cs.spheres += bv.n_big;
   clk.mark(kSecQBig);
@@ -577,7 +580,7 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
                                              const float4* __restrict__ lg32, int hint,
                                              double ox, double oy, double oz, double dx, double dy,
                                              double dz, double A, double& bt, int& bi,
-                                             CS& cs, int& node, unsigned tail) {
+                                             CS& cs, int& node, unsigned tail, double r_check) {
   // Far origins are re-based at their root-box entry o' = o + t0 d (FP64), so
   // the FP32 slab test sees |o'| <= the scene scale and its error bound holds;
   // box intervals are then tested over [-t0, bt - t0]. The exact sphere tests
@@ -585,7 +588,7 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
   double t0 = 0.0;
   const double am = __builtin_fmax(__builtin_fabs(ox),
                                    __builtin_fmax(__builtin_fabs(oy), __builtin_fabs(oz)));
-  if (!(am <= bv.r_check)) t0 = __builtin_fmax(0.0, root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt));
+  if (!(am <= r_check)) t0 = __builtin_fmax(0.0, root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt));
   const float fox = (float)(ox + t0 * dx), foy = (float)(oy + t0 * dy), foz = (float)(oz + t0 * dz);
   const float ix = safe_inv((float)dx), iy = safe_inv((float)dy), iz = safe_inv((float)dz);
   const float oix = fox * ix, oiy = foy * iy, oiz = foz * iz;
@@ -669,11 +672,11 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
   SectionClock<false> noclk;
   const GridC gc = grid_consts(bv);
   if (!hit_quick(geo, geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs, noclk, trapped,
-                 0u, bv.nb_rec, gc, bv.geo32))
+                 0u, bv.nb_rec, gc, bv.geo32, bv.big_idx))
   {
     int node = 0;
     hit_traverse<false, false>(bv, bv.nodes, bv.leaf_idx, geo, bv.geo32, hint, ox, oy, oz, dx,
-                               dy, dz, A, bt, bi, cs, node, 0u);
+                               dy, dz, A, bt, bi, cs, node, 0u, bv.r_check);
   }
   best_t = bt;
   return bi;
@@ -711,13 +714,14 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
   // (previous-hit test, grid cell items, the hit record) then read LDS.
   // (dynamic LDS, sized by the host for this scene: psrt_kernels.h lds_layout)
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
-  const LdsLayout lay = lds_layout(a.n, bv.n_nodes, bv.n_leaf);
+  const LdsLayout lay = lds_layout(a.n, bv.n_nodes, bv.n_leaf, bv.n_big);
   float4* const s_nodes = (float4*)(s_dyn + lay.nodes);
   double4* const s_geo = (double4*)(s_dyn + lay.geo);
   double* const s_inv = (double*)(s_dyn + lay.inv);
   int* const s_leaf = (int*)(s_dyn + lay.leaf);
   uint2* const s_nb = (uint2*)(s_dyn + lay.nb);
   float4* const s_g32 = (float4*)(s_dyn + lay.g32);
+  int* const s_big = (int*)(s_dyn + lay.big);
   // Constants only the refill block reads (camera basis, image size, the
   // divisions' magic numbers, the seed) live in LDS and are re-read on every
   // refill through an offset the compiler cannot see through: held across
@@ -757,6 +761,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
     for (int e = threadIdx.x; e < a.n; e += blockDim.x) s_geo[e] = geo[e], s_inv[e] = inv_r[e];
     for (int e = threadIdx.x; e < bv.n_leaf; e += blockDim.x) s_leaf[e] = bv.leaf_idx[e];
     for (int e = threadIdx.x; e < a.n; e += blockDim.x) s_nb[e] = bv.nb_rec[e], s_g32[e] = bv.geo32[e];
+    for (int e = threadIdx.x; e < bv.n_big; e += blockDim.x) s_big[e] = bv.big_idx[e];
   }
   __syncthreads();
   const float4* __restrict__ nodes = kLds ? s_nodes : bv.nodes;
@@ -765,6 +770,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
   const int* __restrict__ lleaf = kLds ? s_leaf : bv.leaf_idx;
   const uint2* __restrict__ lnb = kLds ? s_nb : bv.nb_rec;
   const float4* __restrict__ lg32 = kLds ? s_g32 : bv.geo32;
+  const int* __restrict__ lbig = kLds ? s_big : bv.big_idx;
 
   // wave-uniform work window
   uint64_t win_base = 0;
@@ -983,7 +989,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
           asm volatile("" : "+v"(zg));  // re-read the grid constants from LDS here
           const GridC& gc = *(const GridC*)((const char*)&s_gc + zg);
           resolved = hit_quick(geo, lgeo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi,
-                               cs, clk, trapped, q, lnb, gc, lg32);
+                               cs, clk, trapped, q, lnb, gc, lg32, lbig);
 #if PSRT_ABLATE == 1
           {
             double bt2;
@@ -991,7 +997,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
             bool tr2;
             CullStatsT<false> cs2{0u, 0u};
             const bool r2 = hit_quick(geo, lgeo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt2,
-                                      bi2, cs2, clk, tr2, q, lnb, gc, lg32);
+                                      bi2, cs2, clk, tr2, q, lnb, gc, lg32, lbig);
             ablate_sink(bt2), ablate_sink(bi2), ablate_sink(tr2), ablate_sink(r2);
           }
 #endif
@@ -1033,19 +1039,24 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
         __builtin_amdgcn_s_setprio(kWalkPrio);
         if (pending) {
           clk.util(kUWalk);
+          // r_check from the grid constants in LDS (held in SGPRs across the
+          // loop it spills, and every use is a v_readlane)
+          unsigned zr = 0;
+          asm volatile("" : "+v"(zr));
+          const double rchk = ((const GridC*)((const char*)&s_gc + zr))->r_check;
 #if PSRT_ABLATE == 2
           {
             double bt2 = pbt;
             int bi2 = pbi, n2 = wnode;
             CullStatsT<false> cs2{0u, 0u};
             hit_traverse<false, kLds>(bv, nodes, lleaf, lgeo, lg32, hint, ox, oy, oz, dx, dy, dz,
-                                      A, bt2, bi2, cs2, n2, movable ? kWalkTail : 0u);
+                                      A, bt2, bi2, cs2, n2, movable ? kWalkTail : 0u, rchk);
             ablate_sink(bt2), ablate_sink(bi2), ablate_sink(n2);
           }
 #endif
           hit_traverse<kStamps, kLds>(bv, nodes, lleaf, lgeo, lg32, hint, ox, oy,
                                                          oz, dx, dy, dz, A, pbt, pbi, cs, wnode,
-                                                         movable ? kWalkTail : 0u);
+                                                         movable ? kWalkTail : 0u, rchk);
           if (wnode >= bv.n_nodes) {
             pending = false;
             resolved = true;
