@@ -115,6 +115,7 @@ struct rt_context {
   psrt::GridHost pgrid;  // point-location grid (host copy of the geometry)
   double pad = 0.0;
   int n_nodes = 0, n_big = 0, n_leaf = 0;
+  int walk0 = 0;  // BvhView::walk0
   double r_check = 0.0;
   hipStream_t stream = nullptr;
   double4* d_geo = nullptr;
@@ -444,10 +445,12 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
   c->d_cell_rec = nullptr, c->d_nb_rec = nullptr;
   c->bvh = b.enabled;
   c->n_nodes = c->n_big = c->n_leaf = 0;
+  c->walk0 = 0;
   if (b.enabled) {
     c->n_nodes = (int)b.nodes.size() - 1;  // the walk's node count (excl. padding)
     c->n_big = (int)b.big_idx.size();
     c->n_leaf = (int)b.leaf_idx.size();
+    c->walk0 = (c->n_nodes > 1 && b.nodes[0].leaf < 0) ? 1 : 0;
     c->r_check = b.r_check;
     std::vector<double4> lg(c->n_leaf);
     for (int k = 0; k < c->n_leaf; ++k) lg[k] = geo[b.leaf_idx[k]];
@@ -510,6 +513,7 @@ static psrt::BvhView bvh_view(const rt_context* c) {
   v.n_nodes = c->n_nodes;
   v.n_big = c->n_big;
   v.n_leaf = c->n_leaf;
+  v.walk0 = c->walk0;
   v.r_check = c->r_check;
   v.cell_start = c->d_cell_start;
   v.cell_items = c->d_cell_items;

@@ -116,6 +116,9 @@ struct BvhView {
   const int* __restrict__ leaf_idx;      // original index per leaf slot
   const int* __restrict__ big_idx;       // spheres tested on every ray
   int n_nodes, n_big, n_leaf;
+  // first node of a walk: 1 when the root is interior (every parked ray is
+  // inside its box, or re-based onto it: testing it is wasted), else 0
+  int walk0;
   double r_check;
   // point-location grid (psrt_bvh.h GridHost)
   const int* __restrict__ cell_start;

@@ -594,7 +594,7 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
   const float oix = fox * ix, oiy = foy * iy, oiz = foz * iz;
   const float tlo = -(float)t0 * 1.00000048f;  // <= -t0: the ray's t >= 0
   float tmax = tmax_up(bt - t0);
-  if constexpr (kDiag) cs.trav_rays += node == 0;
+  if constexpr (kDiag) cs.trav_rays += node == bv.walk0;
   // Two nodes per trip: in DFS skip-link order an interior hit always
   // continues at node+1, so node+1 is loaded alongside node and, when node is
   // an interior hit, box-tested in the same trip; the trip then advances two
@@ -674,7 +674,7 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
   if (!hit_quick(geo, geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs, noclk, trapped,
                  0u, bv.nb_rec, gc, bv.geo32, bv.big_idx))
   {
-    int node = 0;
+    int node = bv.walk0;
     hit_traverse<false, false>(bv, bv.nodes, bv.leaf_idx, geo, bv.geo32, hint, ox, oy, oz, dx,
                                dy, dz, A, bt, bi, cs, node, 0u, bv.r_check);
   }
@@ -1002,7 +1002,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
           }
 #endif
           pending = !resolved;
-          wnode = 0;
+          wnode = bv.walk0;
           if constexpr (kStamps) {
             wbox0 = cs.boxes;
             wfin = pbt < 1e30;

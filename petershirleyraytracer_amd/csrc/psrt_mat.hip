@@ -191,7 +191,7 @@ __device__ __forceinline__ void hit_walk_m(TestCount<kCount>& nt, TestCount<kCou
   // While-while (Aila & Laine 2009): a lane that reaches a leaf holds it
   // until every lane of the wave holds one or is done; the held leaves' FP64
   // tests then run together instead of once per trip in which any lane has one.
-  int node = 0;
+  int node = bv.walk0;  // the root is not tested (psrt_kernels.h BvhView::walk0)
   for (;;) {
     int leaf = -1;
     while (node < bv.n_nodes && leaf < 0) {
