@@ -413,10 +413,11 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
                                           bool& trapped, unsigned q,
                                           const uint2* __restrict__ lnb, const GridC& gc,
                                           const float4* __restrict__ lg32,
-                                          const int* __restrict__ lbig) {
+                                          const int* __restrict__ lbig, float& t0f) {
   bt = __builtin_inf();
   bi = -1;
   trapped = false;
+  t0f = 0.0f;
   const bool finite = (A > 0.0) && (A < 1e200);
   const double am = __builtin_fmax(__builtin_fabs(ox),
                                    __builtin_fmax(__builtin_fabs(oy), __builtin_fabs(oz)));
@@ -561,10 +562,14 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     // miss proves no BVH sphere can have a root in [0, bt]; a hit parks the
     // ray for the batched walk, which re-bases it at the box entry (hit_traverse).
     ++cs.boxes;
-    if (root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt) < 0.0) {
+    const double e = root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt);
+    if (e < 0.0) {
       clk.util(kUFarMiss);
       return true;
     }
+    // the walk re-bases the ray here (hit_traverse); any nearby point of the
+    // ray serves, so the float rounding of the entry is harmless
+    t0f = (float)e;
   }
   clk.util(kUPark);
   return false;
@@ -580,15 +585,15 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
                                              const float4* __restrict__ lg32, int hint,
                                              double ox, double oy, double oz, double dx, double dy,
                                              double dz, double A, double& bt, int& bi,
-                                             CS& cs, int& node, unsigned tail, double r_check) {
+                                             CS& cs, int& node, unsigned tail, double t0) {
   // Far origins are re-based at their root-box entry o' = o + t0 d (FP64), so
   // the FP32 slab test sees |o'| <= the scene scale and its error bound holds;
   // box intervals are then tested over [-t0, bt - t0]. The exact sphere tests
   // in the leaves keep the original o.
-  double t0 = 0.0;
+  // t0: the entry hit_quick found (0 for near origins); a resumed walk keeps
+  // it (a smaller bt only shortens [-t0, bt - t0])
   const double am = __builtin_fmax(__builtin_fabs(ox),
                                    __builtin_fmax(__builtin_fabs(oy), __builtin_fabs(oz)));
-  if (!(am <= r_check)) t0 = __builtin_fmax(0.0, root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt));
   const float fox = (float)(ox + t0 * dx), foy = (float)(oy + t0 * dy), foz = (float)(oz + t0 * dz);
   const float ix = safe_inv((float)dx), iy = safe_inv((float)dy), iz = safe_inv((float)dz);
   const float oix = fox * ix, oiy = foy * iy, oiz = foz * iz;
@@ -671,12 +676,13 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
   bool trapped;
   SectionClock<false> noclk;
   const GridC gc = grid_consts(bv);
+  float t0f;
   if (!hit_quick(geo, geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs, noclk, trapped,
-                 0u, bv.nb_rec, gc, bv.geo32, bv.big_idx))
+                 0u, bv.nb_rec, gc, bv.geo32, bv.big_idx, t0f))
   {
     int node = bv.walk0;
     hit_traverse<false, false>(bv, bv.nodes, bv.leaf_idx, geo, bv.geo32, hint, ox, oy, oz, dx,
-                               dy, dz, A, bt, bi, cs, node, 0u, bv.r_check);
+                               dy, dz, A, bt, bi, cs, node, 0u, (double)t0f);
   }
   best_t = bt;
   return bi;
@@ -791,6 +797,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
   unsigned wbox0 = 0;    // diagnostic build: box tests before this ray's walk
   bool wfin = false;     // diagnostic build: the parked ray had a finite bound
   int wnode = 0;         // where the parked ray's walk resumes
+  float wt0 = 0.0f;      // its re-basing point: the root-box entry of a far origin (hit_quick), else 0
   bool sc_wait = false;  // hit resolved (pbi, pbt), scatter waits for a queued trial
   // look-ahead of random_in_unit_sphere (vec3.h:83-95): accepted trials, in
   // stream order, as raw rand() triples (z, y, x draw order)
@@ -989,15 +996,16 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
           asm volatile("" : "+v"(zg));  // re-read the grid constants from LDS here
           const GridC& gc = *(const GridC*)((const char*)&s_gc + zg);
           resolved = hit_quick(geo, lgeo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi,
-                               cs, clk, trapped, q, lnb, gc, lg32, lbig);
+                               cs, clk, trapped, q, lnb, gc, lg32, lbig, wt0);
 #if PSRT_ABLATE == 1
           {
             double bt2;
             int bi2;
             bool tr2;
             CullStatsT<false> cs2{0u, 0u};
+            float t02;
             const bool r2 = hit_quick(geo, lgeo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt2,
-                                      bi2, cs2, clk, tr2, q, lnb, gc, lg32, lbig);
+                                      bi2, cs2, clk, tr2, q, lnb, gc, lg32, lbig, t02);
             ablate_sink(bt2), ablate_sink(bi2), ablate_sink(tr2), ablate_sink(r2);
           }
 #endif
@@ -1039,24 +1047,19 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
         __builtin_amdgcn_s_setprio(kWalkPrio);
         if (pending) {
           clk.util(kUWalk);
-          // r_check from the grid constants in LDS (held in SGPRs across the
-          // loop it spills, and every use is a v_readlane)
-          unsigned zr = 0;
-          asm volatile("" : "+v"(zr));
-          const double rchk = ((const GridC*)((const char*)&s_gc + zr))->r_check;
 #if PSRT_ABLATE == 2
           {
             double bt2 = pbt;
             int bi2 = pbi, n2 = wnode;
             CullStatsT<false> cs2{0u, 0u};
             hit_traverse<false, kLds>(bv, nodes, lleaf, lgeo, lg32, hint, ox, oy, oz, dx, dy, dz,
-                                      A, bt2, bi2, cs2, n2, movable ? kWalkTail : 0u, rchk);
+                                      A, bt2, bi2, cs2, n2, movable ? kWalkTail : 0u, (double)wt0);
             ablate_sink(bt2), ablate_sink(bi2), ablate_sink(n2);
           }
 #endif
           hit_traverse<kStamps, kLds>(bv, nodes, lleaf, lgeo, lg32, hint, ox, oy,
                                                          oz, dx, dy, dz, A, pbt, pbi, cs, wnode,
-                                                         movable ? kWalkTail : 0u, rchk);
+                                                         movable ? kWalkTail : 0u, (double)wt0);
           if (wnode >= bv.n_nodes) {
             pending = false;
             resolved = true;
