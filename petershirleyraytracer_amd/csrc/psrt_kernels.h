@@ -35,19 +35,26 @@ constexpr int kShardStride = 16;       // u64 words between heads / counter sets
 // many workgroups per CU stay resident as without (C3: 573 nodes, 485
 // spheres, 41.6 KB; three workgroups).
 struct LdsLayout {
-  unsigned nodes, geo, inv, leaf, nb, g32, big, bytes;
+  unsigned nodes, sph, leaf, big, bytes;
 };
+// One 64-B record per sphere (r04): the sphere {c, r*r}, its FP32 pre-reject
+// sphere (BvhView::geo32), its neighbour record (BvhView::nb_rec) and 1/r, so
+// a sphere's fields share one base register and one index computation.
+struct LdsSphere {
+  double4 geo;
+  float4 g32;
+  uint2 nb;
+  double inv;
+};
+static_assert(sizeof(LdsSphere) == 64, "LDS sphere record");
 __host__ __device__ inline LdsLayout lds_layout(int n, int n_nodes, int n_leaf, int n_big) {
   auto a16 = [](unsigned x) { return (x + 15u) & ~15u; };
   LdsLayout l;
-  l.nodes = 0;
-  l.geo = 32u * (unsigned)(n_nodes + 1);
-  l.inv = l.geo + 32u * (unsigned)n;
-  l.leaf = a16(l.inv + 8u * (unsigned)n);
-  l.nb = a16(l.leaf + 4u * (unsigned)n_leaf);
-  l.g32 = a16(l.nb + 8u * (unsigned)n);  // nb: BvhView::nb_rec
-  l.big = a16(l.g32 + 16u * (unsigned)n);  // g32: BvhView::geo32
-  l.bytes = a16(l.big + 4u * (unsigned)(n_big > 0 ? n_big : 1));  // big: BvhView::big_idx
+  l.nodes = 0;                                 // the walk's array at a constant address
+  l.sph = 32u * (unsigned)(n_nodes + 1);       // LdsSphere [n]
+  l.leaf = l.sph + 64u * (unsigned)n;          // leaf slots [n_leaf]
+  l.big = a16(l.leaf + 4u * (unsigned)n_leaf);  // big-sphere indices [n_big]
+  l.bytes = a16(l.big + 4u * (unsigned)(n_big > 0 ? n_big : 1));
   return l;
 }
 

@@ -386,6 +386,30 @@ __device__ __forceinline__ bool first_active_lane() {
   return __lane_id() == (unsigned)__builtin_ctzll(__ballot(1));
 }
 
+// Per-sphere data as the trace loop reads it: one LdsSphere record per sphere
+// in LDS (kLds; psrt_kernels.h), else the separate global arrays.
+template <bool kRec>
+struct SphereView;
+template <>
+struct SphereView<true> {
+  const LdsSphere* __restrict__ s;
+  __device__ double4 geo(int i) const { return s[i].geo; }
+  __device__ float4 g32(int i) const { return s[i].g32; }
+  __device__ uint2 nb(int i) const { return s[i].nb; }
+  __device__ double inv(int i) const { return s[i].inv; }
+};
+template <>
+struct SphereView<false> {
+  const double4* __restrict__ g;
+  const float4* __restrict__ f;
+  const uint2* __restrict__ b;
+  const double* __restrict__ v;
+  __device__ double4 geo(int i) const { return g[i]; }
+  __device__ float4 g32(int i) const { return f[i]; }
+  __device__ uint2 nb(int i) const { return b[i]; }
+  __device__ double inv(int i) const { return v[i]; }
+};
+
 // Cheap part of hittable_list::hit with culling: the previous-hit sphere
 // first, the big spheres, then the point-location grid. Returns true when the
 // closest hit is decided (bt, bi); false when the BVH must be walked (the
@@ -404,16 +428,15 @@ __device__ __forceinline__ bool first_active_lane() {
 // guards keep hb far from under/overflow for every reachable direction
 // d = ((p + n) + rv) - p (n = +-(o - c)/r, rv in n's hemisphere, so
 // |hb| >= r/2): 2^-700 <= r^2 <= 2^700 and |o|_inf <= 2^40.
-template <class Clock, class CS>
+template <class Clock, class CS, class SV>
 __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
-                                          const double4* __restrict__ lgeo, int n,
+                                          const SV& sv, int n,
                                           const BvhView& bv, int hint, double ox, double oy,
                                           double oz, double dx, double dy, double dz, double A,
                                           double& bt, int& bi, CS& cs, Clock& clk,
                                           bool& trapped, unsigned q,
-                                          const uint2* __restrict__ lnb, const GridC& gc,
-                                          const float4* __restrict__ lg32,
-                                          const int* __restrict__ lbig, float& t0f) {
+                                          const GridC& gc, const int* __restrict__ lbig,
+                                          float& t0f) {
   bt = __builtin_inf();
   bi = -1;
   trapped = false;
@@ -436,7 +459,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
   if (hint < 0 && gc.plist) rec = gc.plist[q];  // from LDS (GridC), not a spilled SGPR pair
   if (hint >= 0) {
     clk.util(kUHint);
-    const double4 sh = lgeo[hint];
+    const double4 sh = sv.geo(hint);
     double ch;
     // the ray's first test: bt = +inf, so no pre-reject
     test_sphere<false>(sh, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, float4{}, pr, &ch);
@@ -462,7 +485,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     // so its centre lies within r_j + r_k + pad of c_j: it is j's neighbour.
     if (bi == hint && am <= gc.r_check && gc.nb_c2 >= 0.0 &&
         (ch <= 0.0 || ch * ch <= gc.nb_c2 * sh.w)) {
-      const uint2 nr = lnb[hint];
+      const uint2 nr = sv.nb(hint);
       nb = (nr.x & 0xFFFFu) != kCamOverflow;
       if (nb) rec = make_uint4(nr.x, nr.y, 0u, 0u);
     }
@@ -476,7 +499,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     for (int b = 0; b < bv.n_big; ++b) {
       const int idx = lbig[b];
       if (idx != hint)
-        f2 |= test_sphere(lgeo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt2, bi2, lg32[idx], pr);
+        f2 |= test_sphere(sv.geo(idx), idx, ox, oy, oz, dx, dy, dz, A, bt2, bi2, sv.g32(idx), pr);
     }
     ablate_sink(bt2), ablate_sink(bi2), ablate_sink(f2);
   }
@@ -486,7 +509,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
   for (int b = 0; b < bv.n_big; ++b) {
     const int idx = lbig[b];
     if (idx != hint)
-      full |= test_sphere(lgeo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi, lg32[idx], pr);
+      full |= test_sphere(sv.geo(idx), idx, ox, oy, oz, dx, dy, dz, A, bt, bi, sv.g32(idx), pr);
   }
   cs.spheres += bv.n_big;
   clk.mark(kSecQBig);
@@ -537,7 +560,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
       hi2 >>= 16;
       const int idx = (int)(lo2 & 0xFFFFu);
       if (idx == hint) continue;
-      f2 |= test_sphere(lgeo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt2, bi2, lg32[idx], pr);
+      f2 |= test_sphere(sv.geo(idx), idx, ox, oy, oz, dx, dy, dz, A, bt2, bi2, sv.g32(idx), pr);
     }
     ablate_sink(bt2), ablate_sink(bi2), ablate_sink(f2);
   }
@@ -548,7 +571,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     hi >>= 16;
     const int idx = (int)(lo & 0xFFFFu);
     if (idx == hint) continue;
-    full |= test_sphere(lgeo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi, lg32[idx], pr);
+    full |= test_sphere(sv.geo(idx), idx, ox, oy, oz, dx, dy, dz, A, bt, bi, sv.g32(idx), pr);
   }
   cs.spheres += cnt;
   clk.mark(kSecQGrid);
@@ -578,11 +601,10 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
 
 // The BVH walk (stackless, skip links) for a bounded ray, continuing from the
 // (bt, bi) hit_quick left.
-template <bool kDiag, bool kLdsLeaves, class CS>
+template <bool kDiag, bool kLdsLeaves, class CS, class SV>
 __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __restrict__ nodes,
-                                             const int* __restrict__ leaf_idx,
-                                             const double4* __restrict__ lgeo,
-                                             const float4* __restrict__ lg32, int hint,
+                                             const int* __restrict__ leaf_idx, const SV& sv,
+                                             int hint,
                                              double ox, double oy, double oz, double dx, double dy,
                                              double dz, double A, double& bt, int& bi,
                                              CS& cs, int& node, unsigned tail, double t0) {
@@ -656,8 +678,8 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
       for (int k = first; k < first + cnt; ++k) {
         const int idx = leaf_idx[k];
         if (idx == hint) continue;
-        test_sphere(kLdsLeaves ? lgeo[idx] : bv.leaf_geo[k], idx, ox, oy, oz, dx, dy, dz, A, bt,
-                    bi, lg32[idx], pr);
+        test_sphere(kLdsLeaves ? sv.geo(idx) : bv.leaf_geo[k], idx, ox, oy, oz, dx, dy, dz, A, bt,
+                    bi, sv.g32(idx), pr);
         ++cs.spheres;
       }
       tmax = tmax_up(bt - t0);
@@ -677,12 +699,13 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
   SectionClock<false> noclk;
   const GridC gc = grid_consts(bv);
   float t0f;
-  if (!hit_quick(geo, geo, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs, noclk, trapped,
-                 0u, bv.nb_rec, gc, bv.geo32, bv.big_idx, t0f))
+  const SphereView<false> sv{geo, bv.geo32, bv.nb_rec, nullptr};
+  if (!hit_quick(geo, sv, n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, cs, noclk, trapped,
+                 0u, gc, bv.big_idx, t0f))
   {
     int node = bv.walk0;
-    hit_traverse<false, false>(bv, bv.nodes, bv.leaf_idx, geo, bv.geo32, hint, ox, oy, oz, dx,
-                               dy, dz, A, bt, bi, cs, node, 0u, (double)t0f);
+    hit_traverse<false, false>(bv, bv.nodes, bv.leaf_idx, sv, hint, ox, oy, oz, dx, dy, dz, A, bt,
+                               bi, cs, node, 0u, (double)t0f);
   }
   best_t = bt;
   return bi;
@@ -722,11 +745,8 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   const LdsLayout lay = lds_layout(a.n, bv.n_nodes, bv.n_leaf, bv.n_big);
   float4* const s_nodes = (float4*)(s_dyn + lay.nodes);
-  double4* const s_geo = (double4*)(s_dyn + lay.geo);
-  double* const s_inv = (double*)(s_dyn + lay.inv);
+  LdsSphere* const s_sph = (LdsSphere*)(s_dyn + lay.sph);
   int* const s_leaf = (int*)(s_dyn + lay.leaf);
-  uint2* const s_nb = (uint2*)(s_dyn + lay.nb);
-  float4* const s_g32 = (float4*)(s_dyn + lay.g32);
   int* const s_big = (int*)(s_dyn + lay.big);
   // Constants only the refill block reads (camera basis, image size, the
   // divisions' magic numbers, the seed) live in LDS and are re-read on every
@@ -764,18 +784,21 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
   }
   if constexpr (kLds) {  // the host sized the dynamic LDS by lds_layout
     for (int e = threadIdx.x; e < 2 * (bv.n_nodes + 1); e += blockDim.x) s_nodes[e] = bv.nodes[e];
-    for (int e = threadIdx.x; e < a.n; e += blockDim.x) s_geo[e] = geo[e], s_inv[e] = inv_r[e];
+    for (int e = threadIdx.x; e < a.n; e += blockDim.x) {
+      s_sph[e].geo = geo[e];
+      s_sph[e].g32 = bv.geo32[e];
+      s_sph[e].nb = bv.nb_rec[e];
+      s_sph[e].inv = inv_r[e];
+    }
     for (int e = threadIdx.x; e < bv.n_leaf; e += blockDim.x) s_leaf[e] = bv.leaf_idx[e];
-    for (int e = threadIdx.x; e < a.n; e += blockDim.x) s_nb[e] = bv.nb_rec[e], s_g32[e] = bv.geo32[e];
     for (int e = threadIdx.x; e < bv.n_big; e += blockDim.x) s_big[e] = bv.big_idx[e];
   }
   __syncthreads();
   const float4* __restrict__ nodes = kLds ? s_nodes : bv.nodes;
-  const double4* __restrict__ lgeo = kLds ? s_geo : geo;
-  const double* __restrict__ linv = kLds ? s_inv : inv_r;
   const int* __restrict__ lleaf = kLds ? s_leaf : bv.leaf_idx;
-  const uint2* __restrict__ lnb = kLds ? s_nb : bv.nb_rec;
-  const float4* __restrict__ lg32 = kLds ? s_g32 : bv.geo32;
+  SphereView<kLds> sv;
+  if constexpr (kLds) sv.s = s_sph;
+  else sv = SphereView<false>{geo, bv.geo32, bv.nb_rec, inv_r};
   const int* __restrict__ lbig = kLds ? s_big : bv.big_idx;
 
   // wave-uniform work window
@@ -995,8 +1018,8 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
           unsigned zg = 0;
           asm volatile("" : "+v"(zg));  // re-read the grid constants from LDS here
           const GridC& gc = *(const GridC*)((const char*)&s_gc + zg);
-          resolved = hit_quick(geo, lgeo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi,
-                               cs, clk, trapped, q, lnb, gc, lg32, lbig, wt0);
+          resolved = hit_quick(geo, sv, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi,
+                               cs, clk, trapped, q, gc, lbig, wt0);
 #if PSRT_ABLATE == 1
           {
             double bt2;
@@ -1004,8 +1027,8 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
             bool tr2;
             CullStatsT<false> cs2{0u, 0u};
             float t02;
-            const bool r2 = hit_quick(geo, lgeo, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt2,
-                                      bi2, cs2, clk, tr2, q, lnb, gc, lg32, lbig, t02);
+            const bool r2 = hit_quick(geo, sv, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt2,
+                                      bi2, cs2, clk, tr2, q, gc, lbig, t02);
             ablate_sink(bt2), ablate_sink(bi2), ablate_sink(tr2), ablate_sink(r2);
           }
 #endif
@@ -1052,12 +1075,12 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
             double bt2 = pbt;
             int bi2 = pbi, n2 = wnode;
             CullStatsT<false> cs2{0u, 0u};
-            hit_traverse<false, kLds>(bv, nodes, lleaf, lgeo, lg32, hint, ox, oy, oz, dx, dy, dz,
+            hit_traverse<false, kLds>(bv, nodes, lleaf, sv, hint, ox, oy, oz, dx, dy, dz,
                                       A, bt2, bi2, cs2, n2, movable ? kWalkTail : 0u, (double)wt0);
             ablate_sink(bt2), ablate_sink(bi2), ablate_sink(n2);
           }
 #endif
-          hit_traverse<kStamps, kLds>(bv, nodes, lleaf, lgeo, lg32, hint, ox, oy,
+          hit_traverse<kStamps, kLds>(bv, nodes, lleaf, sv, hint, ox, oy,
                                                          oz, dx, dy, dz, A, pbt, pbi, cs, wnode,
                                                          movable ? kWalkTail : 0u, (double)wt0);
           if (wnode >= bv.n_nodes) {
@@ -1149,7 +1172,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
     sc_wait = want && !have;
 #if PSRT_ABLATE == 4
     if (want && have) {
-      const HitRec h = hit_record_of(lgeo[hit], linv[hit], t, ox, oy, oz, dx, dy, dz);
+      const HitRec h = hit_record_of(sv.geo(hit), sv.inv(hit), t, ox, oy, oz, dx, dy, dz);
       double rx = pm1_raw(q0x), ry = pm1_raw(q0y), rz = pm1_raw(q0z);
       if (!((rx * h.nx + ry * h.ny) + rz * h.nz > 0.0)) rx = -rx, ry = -ry, rz = -rz;
       const double ex = ((h.px + h.nx) + rx) - h.px;
@@ -1161,7 +1184,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
 #endif
     if (want && have) {
       clk.util(kUScatter);
-      const HitRec h = hit_record_of(lgeo[hit], linv[hit], t, ox, oy, oz, dx, dy, dz);
+      const HitRec h = hit_record_of(sv.geo(hit), sv.inv(hit), t, ox, oy, oz, dx, dy, dz);
       // vec3.h:78-81 random(-1, 1) from the queued draws; vec3.h:102-109 flip
       double rx = pm1_raw(q0x), ry = pm1_raw(q0y), rz = pm1_raw(q0z);
       q0x = q1x, q0y = q1y, q0z = q1z;
