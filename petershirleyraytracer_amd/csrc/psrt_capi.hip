@@ -575,11 +575,14 @@ static int check_params(const rt_params* p) {
 static void queue_phases(psrt::TraceArgs& ta, int grid, bool guided) {
   const char* ek = std::getenv("PSRT_QUEUE_K");
   const char* ed = std::getenv("PSRT_QUEUE_D");
-  // two tickets per resident wave per phase for large launches: C3 (96 M
-  // units) one frame at a time 13.64 -> 13.56 ms per step; a strong 1/8
-  // shard (12 M units, frames in flight) prefers one (1.96 vs 1.97 ms)
-  const double k = ek ? std::atof(ek) : (ta.total_units >= (32ull << 20) ? 2.0 : 1.0);
-  const double d = ed ? std::atof(ed) : 4.0;  // 8 before frame pipelining (bench.py)
+  // two tickets per resident wave per phase (C3, 96 M units one frame at a
+  // time: 13.64 -> 13.56 ms per step, r02), and the first ticket size at most
+  // units / (2 x waves): the strong 1/8 shard's 20-frame launch (24 M units)
+  // then starts with 1024-unit tickets instead of 512, and its trace takes
+  // 1.480 instead of 1.503 ms per frame (r04, profiles/r04_queue; larger
+  // launches are capped at 1024 either way)
+  const double k = ek ? std::atof(ek) : 2.0;
+  const double d = ed ? std::atof(ed) : 2.0;
   const uint64_t waves = (uint64_t)grid * (psrt::kTraceBlock / 64);
   unsigned s0 = guided ? psrt::kWorkChunk : psrt::kLinearChunk;
   if (const char* el = std::getenv("PSRT_LINEAR_CHUNK"); el && !guided)  // tuning knob
