@@ -1108,6 +1108,7 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
       ra.accum_stride = acc_stride;
       ra.rgb8_stride = rgb_stride;
       ra.fold_stats = f0 == 0;
+      ra.fast_k = p->max_depth <= 1000;
       ra.heads = c->d_counters + kHeads;
       ra.sets = c->d_counters + kSets;
       ra.totals = c->d_counters + kTotals;

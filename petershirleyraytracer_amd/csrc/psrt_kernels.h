@@ -177,6 +177,9 @@ struct ReduceArgs {
   double* accum;          // [pixels][3] (required unless single chunk + rgb only)
   unsigned char* rgb8;    // [pixels][3] or nullptr (last chunk only)
   int fold_stats;         // block 0 folds the counter sets (one reduce per launch: frame 0's)
+  // every k < 1000 (max_depth <= 1000): 0.5^k is one ldexp, no halving loop,
+  // and a sample's colour is formed without branches (psrt_reduce)
+  int fast_k;
   // psrt_reduce over the frames of a multi-frame launch in ONE launch (r04):
   // blockIdx.y = frame f, whose records start f * frame_units into samp_t /
   // samp_k and whose sums / bytes go to accum + f * accum_stride / rgb8 +

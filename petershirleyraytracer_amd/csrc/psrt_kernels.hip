@@ -1301,6 +1301,24 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
   static_assert(kReduceBlock == 64 && (kReduceTile == 16 || kReduceTile == 32),
                 "tile shape of the loads below");
   auto sum_tile = [&](unsigned T) {
+    if (a.fast_k) {
+      // every k < 1000: sample_colour's operations, with 0.5^k as one ldexp
+      // (exact: the sky is >= 0.5) and black as a select, not a branch; a
+      // black sample adds +0.0, as there
+      for (unsigned j = 0; j < T; ++j) {
+        const double tt = s_t[lane][j];
+        const unsigned kk = s_k[lane][j];
+        const bool blk = kk == kSampleBlack;
+        const double w = 1.0 - tt;
+        const double cr = __builtin_ldexp(w + tt * 0.5, -(int)kk);
+        const double cg = __builtin_ldexp(w + tt * 0.7, -(int)kk);
+        const double cb = __builtin_ldexp(w + tt * 1.0, -(int)kk);
+        r += blk ? 0.0 : cr;
+        g += blk ? 0.0 : cg;
+        b += blk ? 0.0 : cb;
+      }
+      return;
+    }
     for (unsigned j = 0; j < T; ++j) {
       double cr, cg, cb;
       sample_colour(s_t[lane][j], s_k[lane][j], cr, cg, cb);
