@@ -51,7 +51,10 @@ constexpr int kTraceWaves = 6;
 #endif
 constexpr unsigned kRefillMin = PSRT_REFILL_MIN;  // idle lanes that trigger the finish + refill block
 constexpr unsigned kWalkBatch = PSRT_WALK_BATCH;  // parked lanes that trigger a batched BVH pass
-constexpr unsigned kWalkTail = 4;    // a BVH pass stops once this few lanes still walk
+#ifndef PSRT_WALK_TAIL
+#define PSRT_WALK_TAIL 6  // r04 re-sweep (profiles/r04_knobs2): 2 / 4 / 6 / 8
+#endif
+constexpr unsigned kWalkTail = PSRT_WALK_TAIL;  // a BVH pass stops once this few lanes still walk
 #ifndef PSRT_RNG_FILL
 #define PSRT_RNG_FILL 2
 #endif
