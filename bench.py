@@ -455,12 +455,17 @@ def main():
     run = {"dn": depth, "kms": [], "rays": [], "exec": [], "frames": [], "prm": prm}
 
     def ptrs(t, nb):
-        return [t[f].data_ptr() for f in range(nb)]
+        # frame f's block by address arithmetic: t[f].data_ptr() builds a view
+        # per frame, ~10 us each, paid before the batch's first launch
+        base, step = t.data_ptr(), t.stride(0) * t.element_size()
+        return [base + f * step for f in range(nb)]
 
     def launch(i, nb, is_timed):
         """Launch i of a timed() sequence: nb frames in one rt_render_device_frames."""
         sl = i % run["dn"]
         ctx, st = ctxs[sl], streams[sl]
+        if timeline and is_timed and "tl_call" not in run:
+            run["tl_call"] = time.monotonic_ns()
         if world == 1:
             # write_color's bytes go straight into pinned host memory
             # (main.cc:70,86 emit the image): psrt_reduce stores them across
@@ -526,6 +531,8 @@ def main():
             n -= out[-1]
         return out
 
+    timeline = bool(os.environ.get("PSRT_BENCH_TIMELINE"))
+
     def timed(dn, nwarm, nsteps, b=None, tail=True, count=False):
         """nwarm untimed + nsteps timed frames in launches of up to b frames,
         dn launches in flight; the timed frames start from an idle GPU and end
@@ -541,11 +548,19 @@ def main():
                 barrier()
                 torch.cuda.synchronize(dev)
                 t0 = time.perf_counter()
+                tl0 = time.monotonic_ns()
             retire(i % dn)  # the slot's previous launch must be done
             launch(i, nb, is_timed)
+        if timeline:
+            tl = time.monotonic_ns()
         drain()
         barrier()
         el = time.perf_counter() - t0
+        if timeline:  # PSRT_BENCH_TIMELINE: host clock marks to set beside a kernel trace
+            print(f"timeline t0_ns={tl0} call_ns={run.pop('tl_call', 0)} enqueued_ns={tl} "
+                  f"end_ns={time.monotonic_ns()} "
+                  f"boot_minus_mono_ns={time.clock_gettime_ns(time.CLOCK_BOOTTIME) - time.monotonic_ns()}",
+                  file=sys.stderr)
         if distributed:
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -565,6 +580,15 @@ def main():
                      - (again["total_ms"] - again["kernel_ms"]))
     for k in range(1, depth):
         one(ctxs[k], k)
+    # A context's sample buffer grows to its largest render so far: one
+    # untimed render of B frames per context here, so no timed launch
+    # allocates (with W < B the warmup launch is shorter than a timed one,
+    # and the first timed launch would free and re-allocate B frames' records
+    # inside the timed region: 0.5-0.8 ms, profiles/r04_timeline)
+    if B > 1:
+        for k in range(depth):
+            ctxs[k].render_device_frames(prm, B, ptrs(acc[k], B), None, streams[k].cuda_stream)
+            ctxs[k].sync_stats()
     torch.cuda.synchronize(dev)
 
     # untimed tuning runs (one frame per launch only): every candidate depth
