@@ -68,6 +68,9 @@ struct FastDiv {
 constexpr unsigned short kSampleBlack = 0xFFFFu;
 constexpr int kSampleKCap = 1100;
 constexpr int kReduceBlock = 64;   // psrt_reduce: one wave per 64 pixels
+#ifndef PSRT_REDUCE_NT
+#define PSRT_REDUCE_NT 0  // psrt_reduce: non-temporal sample loads (A/B knob)
+#endif
 #ifndef PSRT_REDUCE_TILE
 #define PSRT_REDUCE_TILE 32
 #endif

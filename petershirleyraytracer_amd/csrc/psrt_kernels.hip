@@ -1339,15 +1339,29 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
       for (int i = 0; i < kLT; ++i) {
         const unsigned p = kPT * i + lane / kLT, j = (lane % kLT) * 2;
         vt[i] = make_double2(0.0, 0.0);
-        if (q0 + p < a.pixels && j < T)
+        if (q0 + p < a.pixels && j < T) {
+#if PSRT_REDUCE_NT
+          typedef double nt2 __attribute__((ext_vector_type(2)));
+          const nt2 x = __builtin_nontemporal_load((const nt2*)(a.samp_t + (size_t)(q0 + p) * S + s0 + j));
+          vt[i] = make_double2(x.x, x.y);
+#else
           vt[i] = *(const double2*)(a.samp_t + (size_t)(q0 + p) * S + s0 + j);
+#endif
+        }
       }
 #pragma unroll
       for (int i = 0; i < kLK; ++i) {
         const unsigned p = kPK * i + lane / kLK, j = (lane % kLK) * 4;
         vk[i] = make_uint2(0u, 0u);
-        if (q0 + p < a.pixels && j < T)
+        if (q0 + p < a.pixels && j < T) {
+#if PSRT_REDUCE_NT
+          typedef unsigned nu2 __attribute__((ext_vector_type(2)));
+          const nu2 x = __builtin_nontemporal_load((const nu2*)(a.samp_k + (size_t)(q0 + p) * S + s0 + j));
+          vk[i] = make_uint2(x.x, x.y);
+#else
           vk[i] = *(const uint2*)(a.samp_k + (size_t)(q0 + p) * S + s0 + j);
+#endif
+        }
       }
     };
     load(0);
