@@ -68,6 +68,10 @@ struct FastDiv {
 constexpr unsigned short kSampleBlack = 0xFFFFu;
 constexpr int kSampleKCap = 1100;
 constexpr int kReduceBlock = 64;   // psrt_reduce: one wave per 64 pixels
+#ifndef PSRT_REDUCE_IN_FLIGHT
+#define PSRT_REDUCE_IN_FLIGHT 2
+#endif
+constexpr unsigned kReduceInFlight = PSRT_REDUCE_IN_FLIGHT;  // psrt_reduce: sample tiles in flight per wave
 #ifndef PSRT_REDUCE_NT
 #define PSRT_REDUCE_NT 0  // psrt_reduce: non-temporal sample loads (A/B knob)
 #endif
