@@ -73,11 +73,26 @@ CONFIGS = {
 PEAK_FP64_OPS = 256 * 64 * 2.4e9
 PEAK_HBM = 8.0e12
 # sphere.cc:6-14 per ray-sphere test: amc (3), A (5), HALF_B (5), C (5 + r*r + sub = 7),
-# discriminant (3) = 23 FP64 ops. psrt_trace executes 17 of them per test (A is
-# hoisted per ray, r*r per sphere: the same values) + 1 compare.
+# discriminant (3) = 23 FP64 ops (the reference-equivalent figure).
 OPS_PER_TEST = 23
-EXEC_OPS_PER_TEST = 18
-BOX_OPS_FP64_EQ = 7  # FP32 slab test: 6 FMA + 7 min/max + compare = 14 FP32 ops
+# Algorithmic work of psrt_trace as executed, by the kind of test that ran
+# (the counting variant's tallies, RT_FLAG_CULL_STATS), each weighted by its
+# operations' measured issue cost in FP64-op slots: one slot = one FP64 add,
+# 4.4 SIMD cycles per wave64 instruction (scripts/isa_rates.hip; the peak
+# below counts one slot per lane per cycle). Costs (cycles): FP64 add / mul /
+# min / max 4.4, FP64 compare 4.2, v_rcp_f64 16.3, FP32 add / sub 2.35, FP32
+# mul / FMA / min / max / compare 4.25, cvt f64 -> f32 4.2. DESIGN.md §7.
+#   full FP64 sphere test (sphere.cc:6-14 with A hoisted per ray and r*r per
+#     sphere, the same values): 17 FP64 add/mul + 1 compare = 79.0 cycles
+#   FP32 pre-reject (Pre32): 4 add/sub + 5 mul/FMA + 1 compare + 1 cvt = 39.1
+#   FP32 slab test (slab_hit): 6 FMA + 10 min/max + 1 compare = 72.25
+#   FP64 root-box test (root_box_entry): 3 x (compare, v_rcp_f64, 4 add/mul,
+#     4 min/max) + 2 FP64 ops + compare = 180.3
+ISA_CYCLES_PER_SLOT = 4.4
+WEIGHTS = {"full_sphere_test": (17 * 4.4 + 4.2) / 4.4,
+           "prereject": (4 * 2.35 + 5 * 4.25 + 4.25 + 4.2) / 4.4,
+           "box_test": 17 * 4.25 / 4.4,
+           "root_box_test": (3 * (4.2 + 16.3 + 8 * 4.4) + 2 * 4.4 + 4.2) / 4.4}
 # FP64 ops per traced ray outside the sphere/box tests (estimate from the
 # kernel source): hit record 18 (ray.h:25-28, sphere.cc:34-36, hittable.h:14-18),
 # scatter 26 (vec3.h:102-109, main.cc:42-43, the new ray's A), look-ahead
@@ -307,8 +322,12 @@ def profile_counters(config: str):
     """From the committed rocprofv3 PMC summary (profiles/pmc_<config>.json):
     HBM bytes per psrt_trace launch (FETCH_SIZE doubled per the gfx950
     calibration note in MI355X_MICROARCH.md §HBM, + WRITE_SIZE) and the VALU
-    issue rate: SIMD cycles per wave64 VALU instruction, (kernel cycles x 1024
-    SIMDs) / SQ_INSTS_VALU, kernel cycles = GRBM_GUI_ACTIVE / 8 XCDs."""
+    issue: SIMD cycles per wave64 VALU instruction, (kernel cycles x 1024
+    SIMDs) / SQ_INSTS_VALU, kernel cycles = GRBM_GUI_ACTIVE / 8 XCDs; rocprof's
+    VALUBusy, SQ_ACTIVE_INST_VALU x 4 / (kernel cycles x 1024) (quad-cycles
+    per wave, so it can pass 1 when 2-cycle instructions overlap); and the
+    VALU pipe's busy fraction from the instruction mix, FP64 instructions at
+    4 cycles and the others at 2 (SIMD32: a wave64 instruction issues in 2)."""
     path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
     if not os.path.exists(path):
         return None, None
@@ -327,6 +346,19 @@ def profile_counters(config: str):
                     simd_cycles_per_valu_inst=round(cycles * 1024 / c["SQ_INSTS_VALU"], 3),
                     note="a wave64 FP64 VALU op holds a SIMD 4 cycles (16 lanes/cycle)",
                     source=f"profiles/pmc_{config}.json")
+        simd_cycles = cycles * 1024
+        if "SQ_ACTIVE_INST_VALU" in c:
+            valu["valu_busy_rocprof"] = round(c["SQ_ACTIVE_INST_VALU"] * 4 / simd_cycles, 4)
+        f64 = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                          "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
+        if f64:
+            valu["valu_pipe_busy_mix"] = round((4 * f64 + 2 * (c["SQ_INSTS_VALU"] - f64))
+                                               / simd_cycles, 4)
+        if "SQ_THREAD_CYCLES_VALU" in c and "SQ_ACTIVE_INST_VALU" in c:
+            # lanes active per VALU instruction (SIMT divergence): thread-cycles /
+            # (64 x instruction quad-cycles x 4)
+            valu["lane_utilisation"] = round(c["SQ_THREAD_CYCLES_VALU"]
+                                             / (64.0 * c["SQ_ACTIVE_INST_VALU"]), 4)
     except Exception:
         valu = None
     return traffic, valu
@@ -401,7 +433,7 @@ def main():
     # unit ids, the sample buffer and kMaxFrames (32) allow; frames of several
     # sample chunks (C4, C5 on one GPU) go one per launch.
     per_rank = rows * w * spp
-    buf_cap = int(os.environ.get("PSRT_SAMPLE_BUF_MB", "49152")) << 20  # psrt_capi.hip
+    buf_cap = int(P.get_tuning("sample_buf_mb")) << 20  # the library's sample-buffer cap
     multi_chunk = per_rank * SAMPLE_RECORD_BYTES > buf_cap or per_rank >= (1 << 30)
     if args.batch > 0:
         B = min(args.batch, 32)
@@ -517,7 +549,8 @@ def main():
             run["kms"].append(st["kernel_ms"])
             run["rays"].append(st["rays"])
             run["frames"].append(nb)
-            run["exec"].append((st["tests_executed"], st["box_tests"], st["rays_traced"], nb))
+            run["exec"].append((st["tests_executed"], st["box_tests"], st["rays_traced"], nb,
+                                st["prerejects"], st["root_box_tests"]))
 
     def drain():
         for k in range(depth):
@@ -702,15 +735,18 @@ def main():
         avg_ms = float(kernel_ms)  # psrt_trace device time per frame (launch / frames in it)
         rays_launch = float(rays)  # this rank's reference rays per frame
         tests = rays_launch * n  # sphere::hit calls of the reference algorithm
-        ex_tests = float(np.sum([e[0] for e in executed])) / sum(e[3] for e in executed)
-        ex_boxes = float(np.sum([e[1] for e in executed])) / sum(e[3] for e in executed)
-        ex_rays = float(np.sum([e[2] for e in executed])) / sum(e[3] for e in executed)
-        # Algorithmic FP64 work of psrt_trace as executed, in FP64-op slots: 18
-        # per exact sphere test (17 FP64 ops + compare: the reference's 23-op
-        # test with A hoisted per ray and r*r per sphere, identical values), 7
-        # per FP32 box test (14 FP32 ops at twice the FP64 rate) and ~61 per
-        # traced ray for the hit record, scatter and RNG trials.
-        ex_ops = (ex_tests * EXEC_OPS_PER_TEST + ex_boxes * BOX_OPS_FP64_EQ
+        nfr = sum(e[3] for e in executed)
+        ex_tests = float(np.sum([e[0] for e in executed])) / nfr  # full FP64 sphere tests
+        ex_boxes = float(np.sum([e[1] for e in executed])) / nfr  # slab tests evaluated
+        ex_rays = float(np.sum([e[2] for e in executed])) / nfr
+        ex_pre = float(np.sum([e[4] for e in executed])) / nfr    # FP32 pre-rejects
+        ex_root = float(np.sum([e[5] for e in executed])) / nfr   # FP64 root-box tests
+        # Algorithmic work of psrt_trace as executed, in FP64-op slots: each
+        # kind of test that ran at its operations' measured issue cost
+        # (WEIGHTS), plus ~61 FP64 ops per traced ray for the hit record,
+        # scatter and RNG trials.
+        ex_ops = (ex_tests * WEIGHTS["full_sphere_test"] + ex_pre * WEIGHTS["prereject"]
+                  + ex_boxes * WEIGHTS["box_test"] + ex_root * WEIGHTS["root_box_test"]
                   + ex_rays * SHADE_OPS_PER_RAY)
         achieved = ex_ops / (avg_ms * 1e-3)
         ref_equiv = tests * OPS_PER_TEST / (avg_ms * 1e-3)
@@ -749,21 +785,25 @@ def main():
                 "rays_per_launch": int(rays_launch),
                 "rays_traced_per_launch": int(ex_rays),
                 "reference_sphere_tests_per_launch": int(tests),
-                "executed_sphere_tests_per_launch": int(ex_tests),
-                "executed_box_tests_per_launch": int(ex_boxes),
-                "ops_per_sphere_test": EXEC_OPS_PER_TEST,
-                "ops_per_box_test_fp64_eq": BOX_OPS_FP64_EQ,
+                "full_sphere_tests_per_launch": int(ex_tests),
+                "prerejects_per_launch": int(ex_pre),
+                "box_tests_evaluated_per_launch": int(ex_boxes),
+                "root_box_tests_per_launch": int(ex_root),
+                "issue_weights_fp64_slots": {k: round(v, 3) for k, v in WEIGHTS.items()},
                 "reference_ops_per_test": OPS_PER_TEST,
                 "reference_equivalent_tflops": round(ref_equiv / 1e12, 4),
                 "culling": "off (linear sweep)" if (args.no_cull or ex_boxes == 0) else "bvh",
                 "shade_ops_per_traced_ray": SHADE_OPS_PER_RAY,
                 "fixpoint": not args.no_fixpoint,
                 "note": ("VALU-issue bound (FP64 non-FMA op peak 256 CU x 64 lanes x 2.4 GHz); "
-                         "achieved = (executed sphere tests x 18 + box tests x 7 + traced rays "
-                         "x 61) FP64-op slots / avg psrt_trace launch; integer RNG, traversal "
-                         "control and SIMT divergence not counted; rays_per_launch = the "
-                         "reference's rays, rays_traced = those not proven to end black "
-                         "(DESIGN.md 9); reference_equivalent = rays x spheres x 23 / launch"),
+                         "achieved = (full FP64 sphere tests, FP32 pre-rejects, FP32 slab tests "
+                         "evaluated and FP64 root-box tests, each x its issue_weights_fp64_slots "
+                         "(measured instruction costs, scripts/isa_rates.hip), + traced rays x "
+                         "61) / avg psrt_trace launch; integer RNG, traversal control and SIMT "
+                         "divergence not counted; rays_per_launch = the reference's rays, "
+                         "rays_traced = those not proven to end black (DESIGN.md 9); "
+                         "reference_equivalent = rays x spheres x 23 / launch; valu_issue: the "
+                         "PMC issue rates of the same kernel (profiles/pmc_<config>.json)"),
                 "hbm_algorithmic_bytes_per_launch": hbm_alg,
                 "hbm_frac": round(hbm_alg / (avg_ms * 1e-3) / PEAK_HBM, 6),
                 # measured issue rate (PMC) of the same kernel: the SIMDs' VALU

@@ -13,6 +13,7 @@
 // packing every sphere's (centre, radius) — any other hittable is an error.
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <ostream>
 #include <stdexcept>
@@ -90,6 +91,64 @@ inline frame render(const hittable_list& world, const camera& cam, int width, in
                   &f.stats),
         "rt_render");
   return f;
+}
+
+// ---- several devices (rt_group, include/rt.h) --------------
+// One context and one host thread per member; interleaved rows gathered into
+// reference pixel order in host memory; the same bits for any member count.
+//
+//   psrt::device_group g({0, 1, 2, 3, 4, 5, 6, 7});   // one member per GPU
+//   g.set_scene(world, cam);
+//   psrt::frame f = g.render(3840, 2160, 500, 50);    // repeat with new seeds
+class device_group {
+ public:
+  explicit device_group(const std::vector<int>& devices) {
+    check(rt_group_create(devices.data(), (int)devices.size(), &g_), "rt_group_create");
+  }
+  ~device_group() { rt_group_destroy(g_); }
+  device_group(const device_group&) = delete;
+  device_group& operator=(const device_group&) = delete;
+  int size() const { return rt_group_size(g_); }
+  rt_context* context(int member) { return rt_group_context(g_, member); }
+  void set_scene(const std::vector<rt_sphere>& spheres, const rt_camera& cam) {
+    check(rt_group_set_scene(g_, spheres.data(), (int)spheres.size(), &cam), "rt_group_set_scene");
+  }
+  void set_scene(const hittable_list& world, const camera& cam) {
+    set_scene(flatten(world), to_rt(cam));
+  }
+  frame render(int width, int height, int spp, int max_depth, uint64_t seed = 0,
+               int row_offset = 0, int row_stride = 1, unsigned flags = 0) {
+    rt_params p{};
+    p.width = width;
+    p.height = height;
+    p.spp = spp;
+    p.max_depth = max_depth;
+    p.seed = seed;
+    p.row_offset = row_offset;
+    p.row_stride = row_stride;
+    p.flags = flags;
+    frame f;
+    f.width = width;
+    f.height = height;
+    f.spp = spp;
+    f.rows = std::max(0, rt_rows_owned(height, row_offset, row_stride));
+    f.accum.resize((size_t)f.rows * width * 3);
+    f.rgb8.resize((size_t)f.rows * width * 3);
+    check(rt_group_render(g_, &p, f.accum.data(), f.rgb8.data(), &f.stats), "rt_group_render");
+    return f;
+  }
+
+ private:
+  rt_group* g_ = nullptr;
+};
+
+// main.cc:72-88 over several devices (one-shot: the group lives for one frame)
+inline frame render(const hittable_list& world, const camera& cam, int width, int height,
+                    int spp, int max_depth, const std::vector<int>& devices, uint64_t seed = 0,
+                    int row_offset = 0, int row_stride = 1) {
+  device_group g(devices);
+  g.set_scene(world, cam);
+  return g.render(width, height, spp, max_depth, seed, row_offset, row_stride);
 }
 
 // The book's material integrator and thin lens (extension):

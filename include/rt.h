@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 /* ---- error codes ---------------------------------------------------------- */
 #define RT_OK 0
@@ -86,9 +86,9 @@ typedef struct {
 /* scheduling hint, same bits: the launch's draining waves do not take issue
  * priority over other work (e.g. the next frame's launch on another stream) */
 #define RT_FLAG_NO_TAIL_PRIORITY 4u
-/* count the sphere / box tests the device runs (rt_stats.tests_executed,
- * box_tests) with a slower kernel variant (~1%); without it both read 0.
- * Same bits; every other counter is always exact. */
+/* count the tests the device runs, by kind (rt_stats.tests_executed,
+ * prerejects, box_tests, root_box_tests), with a slower kernel variant (~1%);
+ * without it they read 0. Same bits; every other counter is always exact. */
 #define RT_FLAG_CULL_STATS 8u
 /* render with the material integrator and lens camera of the context
  * (rt_context_set_materials) instead of the reference's
@@ -111,14 +111,17 @@ typedef struct {
   uint64_t samples;        /* camera samples traced                          */
   uint64_t rays;           /* ray_color() invocations that called world.hit  */
   uint64_t sphere_tests;   /* sphere::hit calls of the reference = rays * n  */
-  uint64_t tests_executed; /* FP64 sphere tests the device ran (culled);
-                              0 without RT_FLAG_CULL_STATS                   */
-  uint64_t box_tests;      /* FP32 BVH box tests the device ran (same)       */
+  uint64_t tests_executed; /* sphere tests the device ran in full, in FP64
+                              (sphere.cc:6-31); 0 without RT_FLAG_CULL_STATS */
+  uint64_t box_tests;      /* FP32 BVH slab tests the device evaluated (same) */
   double kernel_ms;        /* device time of the trace kernels (HIP events)  */
   double total_ms;         /* device time of the whole render                */
   uint64_t rays_traced;    /* of `rays`, those the device traced; the rest
                               are the rays of provably trapped paths, ended
                               early with the same result     */
+  uint64_t prerejects;     /* sphere candidates an exact FP32 pre-reject
+                              decided without the FP64 test (same flag)     */
+  uint64_t root_box_tests; /* FP64 ray / root-box tests of far origins (same) */
 } rt_stats;
 
 /* Number of rows a shard owns. */
@@ -185,6 +188,32 @@ int rt_context_sync_stats(rt_context* ctx, rt_stats* stats);
 /* Device-side write_color over d_accum (rows*width*3) -> d_rgb8. */
 int rt_quantize_device(rt_context* ctx, const double* d_accum, int width,
                        int rows, int spp, unsigned char* d_rgb8, void* stream);
+
+/* ---- several devices, natively (psrt_group.cpp) -----------
+ * One frame over a group of devices with no collective library: member g of
+ * a G-member group renders the rows row_offset + (g + k*G)*row_stride of the
+ * caller's shard on its own rt_context from its own host thread (interleaved
+ * rows keep the load balanced), and copies them straight into their places in
+ * the caller's host buffers: reference pixel order, bit-identical for every
+ * G. Members may name the same device (each has its own context). This is the
+ * C / C++ drop-in's multi-GPU path (one host thread per device); bench.py's is
+ * one process per GPU over RCCL. RT_FLAG_MATERIALS is not supported here. */
+typedef struct rt_group rt_group;
+int rt_group_create(const int* devices, int n_devices, rt_group** out);
+int rt_group_destroy(rt_group* group);
+int rt_group_size(const rt_group* group);
+/* member's context (tuning knobs, stats), or NULL when out of range */
+rt_context* rt_group_context(rt_group* group, int member);
+int rt_group_set_scene(rt_group* group, const rt_sphere* spheres, int n_spheres,
+                       const rt_camera* cam);
+/* accum_rgb / rgb8: host, rows_owned(params) x width x 3 (either may be NULL);
+ * stats: counts summed over members, kernel_ms / total_ms the slowest member's */
+int rt_group_render(rt_group* group, const rt_params* params, double* accum_rgb,
+                    unsigned char* rgb8, rt_stats* stats);
+/* One-shot: rt_group_create + set_scene + render + destroy. */
+int rt_render_devices(const rt_sphere* spheres, int n_spheres, const rt_camera* cam,
+                      const rt_params* params, const int* devices, int n_devices,
+                      double* accum_rgb, unsigned char* rgb8, rt_stats* stats);
 
 /* ---- scene helpers (host) -------------------------------------------------- */
 
@@ -323,9 +352,32 @@ int rt_debug_world_hit(const rt_sphere* spheres, int n_spheres, const double* ra
 int rt_debug_world_hit_hint(const rt_sphere* spheres, int n_spheres, const double* rays,
                             const int* hints, int count, double* out, int cull);
 
+/* ---- tuning (measurement and tests only) ------------------------------------
+ * The render path reads no environment variable. These knobs exist for A/B
+ * measurements and for tests that force a code path; every one keeps the
+ * output bit-identical (only the sample-buffer cap and the diagnostic variant
+ * change anything but time: chunking, and the stamps on stderr).
+ *   sample_buf_mb   cap of the sample-record buffer, MiB (default 49152)
+ *   queue_k, queue_d  guided work-queue shape (2, 2; psrt_capi.hip queue_phases)
+ *   linear_chunk    queue ticket of the small-scene path (0: 1024)
+ *   no_camlist, no_neighbors, no_fixpoint, no_lds  1 disables that exact shortcut
+ *   blocks_per_cu   cap on resident trace workgroups per CU (0: occupancy max)
+ *   mat_lds         material kernel's scene in LDS: -1 auto, 0 off, 1 on
+ *   mat_batch       parked lanes per batched walk of the material kernel (48)
+ *   flush_at        per-lane counter flush threshold (0: computed)
+ *   stamps          1: the diagnostic kernel variant (section clocks on stderr)
+ *   scene_rebuild   1: rebuild the culling structures for an unchanged scene
+ *   big_ratio       radius ratio of the big-sphere class (0: 16)
+ * ctx == NULL sets / reads the process defaults: a context copies them at
+ * rt_context_create, the one-shot entries' default contexts at every call.
+ * Unknown names and non-finite values fail with RT_E_INVALID. */
+int rt_context_set_tuning(rt_context* ctx, const char* name, double value);
+int rt_context_get_tuning(rt_context* ctx, const char* name, double* value);
+
 /* Debug (fault injection, tests only): the context's NEXT render fails with
  * RT_E_HIP after sample chunk `chunk`'s trace launch and before its reduce, as
- * a HIP error there would; the hook then clears itself. chunk < 0 clears it.
+ * a HIP error there would (the reference and the material integrator alike);
+ * the hook then clears itself. chunk < 0 clears it.
  * The failure-recovery path (queue heads and counter sets re-zeroed by the
  * next render) is tested through it. */
 int rt_debug_fail_after_trace(rt_context* ctx, int chunk);

@@ -6,15 +6,17 @@ This Python package is host plumbing over that C ABI: scene/camera helpers,
 one-shot and device-resident renders, PPM output, and the multi-GPU sharding
 used by ``bench.py``. See DESIGN.md.
 """
-from .render import (Context, LensCamera, SceneFile, camera_default, camera_look_at,
+from .render import (Context, DeviceGroup, LensCamera, SceneFile, camera_default, camera_look_at,
                      camera_look_at_lens, device_count, format_scene, load_scene, params,
-                     parse_scene, ppm_p3, probe_f64, quantize, render, render_materials,
+                     parse_scene, ppm_p3, probe_f64, quantize, render, render_devices,
+                     render_materials,
                      rows_owned, save_scene, scene_book_final, scene_random_spheres,
-                     scene_two_spheres, write_ppm)
+                     scene_two_spheres, get_tuning, set_tuning, tuning, write_ppm)
 
 __all__ = [
-    "Context", "LensCamera", "SceneFile", "camera_default", "camera_look_at",
+    "Context", "DeviceGroup", "LensCamera", "SceneFile", "camera_default", "camera_look_at",
     "camera_look_at_lens", "device_count", "format_scene", "load_scene", "params", "parse_scene",
-    "ppm_p3", "probe_f64", "quantize", "render", "render_materials", "rows_owned", "save_scene",
-    "scene_book_final", "scene_random_spheres", "scene_two_spheres", "write_ppm",
+    "ppm_p3", "probe_f64", "quantize", "render", "render_devices", "render_materials", "rows_owned", "save_scene",
+    "scene_book_final", "scene_random_spheres", "scene_two_spheres", "get_tuning", "set_tuning",
+    "tuning", "write_ppm",
 ]

@@ -23,7 +23,9 @@ EXPORTS = [
     "rt_last_error", "rt_abi_version", "rt_device_count", "rt_build_info", "rt_debug_probe_f64",
     "rt_debug_world_hit", "rt_debug_world_hit_hint", "rt_debug_fail_after_trace",
     "rt_camera_look_at_lens", "rt_scene_book_final", "rt_context_set_materials",
-    "rt_render_materials",
+    "rt_render_materials", "rt_context_set_tuning", "rt_context_get_tuning",
+    "rt_group_create", "rt_group_destroy", "rt_group_size", "rt_group_context",
+    "rt_group_set_scene", "rt_group_render", "rt_render_devices",
 ]
 
 
@@ -55,7 +57,8 @@ class RtCameraLens(C.Structure):
 class RtStats(C.Structure):
     _fields_ = [("samples", C.c_uint64), ("rays", C.c_uint64), ("sphere_tests", C.c_uint64),
                 ("tests_executed", C.c_uint64), ("box_tests", C.c_uint64),
-                ("kernel_ms", C.c_double), ("total_ms", C.c_double), ("rays_traced", C.c_uint64)]
+                ("kernel_ms", C.c_double), ("total_ms", C.c_double), ("rays_traced", C.c_uint64),
+                ("prerejects", C.c_uint64), ("root_box_tests", C.c_uint64)]
 
 
 class RtError(RuntimeError):
@@ -134,6 +137,17 @@ def load(build_if_missing: bool = False):
                                      C.c_int),
         "rt_render_materials": ([P(RtSphere), P(RtMaterial), C.c_int, P(RtCameraLens),
                                  P(RtParams), P(C.c_double), P(C.c_ubyte), P(RtStats)], C.c_int),
+        "rt_context_set_tuning": ([C.c_void_p, C.c_char_p, C.c_double], C.c_int),
+        "rt_context_get_tuning": ([C.c_void_p, C.c_char_p, P(C.c_double)], C.c_int),
+        "rt_group_create": ([P(C.c_int), C.c_int, P(C.c_void_p)], C.c_int),
+        "rt_group_destroy": ([C.c_void_p], C.c_int),
+        "rt_group_size": ([C.c_void_p], C.c_int),
+        "rt_group_context": ([C.c_void_p, C.c_int], C.c_void_p),
+        "rt_group_set_scene": ([C.c_void_p, P(RtSphere), C.c_int, P(RtCamera)], C.c_int),
+        "rt_group_render": ([C.c_void_p, P(RtParams), P(C.c_double), P(C.c_ubyte), P(RtStats)],
+                            C.c_int),
+        "rt_render_devices": ([P(RtSphere), C.c_int, P(RtCamera), P(RtParams), P(C.c_int),
+                               C.c_int, P(C.c_double), P(C.c_ubyte), P(RtStats)], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

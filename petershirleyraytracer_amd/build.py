@@ -27,7 +27,8 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 # every x*y+z to stay a separate multiply and add.
 COMMON = ["-O3", "-ffp-contract=off", "-std=c++17", "-Wall"]
 
-LIB_SOURCES = ["psrt_kernels.hip", "psrt_mat.hip", "psrt_capi.hip", "psrt_scene.cpp", "psrt_scenefile.cpp", "psrt_bvh.cpp"]
+LIB_SOURCES = ["psrt_kernels.hip", "psrt_mat.hip", "psrt_capi.hip", "psrt_group.cpp", "psrt_scene.cpp",
+               "psrt_scenefile.cpp", "psrt_bvh.cpp"]
 HOST_SOURCES = [os.path.join("host", "raytracer_main.cc")]
 
 

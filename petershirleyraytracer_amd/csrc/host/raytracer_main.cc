@@ -6,6 +6,10 @@
 //   raytracer                       # main.cc as written: 400 wide, 16:9, 100 spp, depth 50
 //   raytracer --scene final --width 1200 --height 800 --spp 100 -o out.ppm
 //   raytracer --rows 1:8 ...        # one interleaved shard (rows 1, 9, 17, ...)
+//   raytracer --devices 8 ...       # one frame over GPUs 0..7 (rt_group: a host
+//                                   # thread and context per device, interleaved
+//                                   # rows); --devices 0,0,1 lists members
+//                                   # explicitly (a device may repeat)
 //   raytracer --scene-file s.scene  # world/camera/parameters from a scene file;
 //                                   # flags given on the command line win
 //   raytracer --scene final --save-scene final.scene   # write the scene, render nothing
@@ -17,6 +21,7 @@
 #include <fstream>
 #include <iostream>
 #include <string>
+#include <vector>
 
 #include "psrt/render.hpp"
 #include "raytracer/camera.h"
@@ -49,8 +54,28 @@ int usage() {
   std::fprintf(stderr,
                "raytracer [--scene two|final|book | --scene-file FILE] [--width W] [--height H]\n"
                "          [--spp S] [--depth D] [--seed N] [--rows OFF:STRIDE] [-o FILE] [--p6]\n"
-               "          [--accum FILE] [--save-scene FILE] [--aperture A] [--focus F]\n");
+               "          [--accum FILE] [--save-scene FILE] [--aperture A] [--focus F]\n"
+               "          [--devices N | --devices D0,D1,...]\n");
   return 2;
+}
+
+// --devices: "N" = devices 0..N-1; "a,b,c" = those members (repeats allowed)
+bool parse_devices(const std::string& v, std::vector<int>& out) {
+  out.clear();
+  if (v.find(',') == std::string::npos) {
+    const int n = std::atoi(v.c_str());
+    if (n < 1) return false;
+    for (int d = 0; d < n; ++d) out.push_back(d);
+    return true;
+  }
+  size_t a = 0;
+  while (a <= v.size()) {
+    const size_t b = std::min(v.find(',', a), v.size());
+    if (b == a) return false;
+    out.push_back(std::atoi(v.substr(a, b - a).c_str()));
+    a = b + 1;
+  }
+  return !out.empty();
 }
 
 }  // namespace
@@ -60,6 +85,7 @@ int main(int argc, char** argv) {
   int width = 400, height = -1, spp = 100, depth = 50, row_off = 0, row_stride = 1;
   unsigned long long seed = 0;
   double aperture = 0.1, focus = 10.0;  // --scene book: the book's lens
+  std::vector<int> devices;             // --devices: several members (rt_group)
   bool p6 = false, set_w = false, set_h = false, set_spp = false, set_depth = false,
        set_seed = false;
   for (int a = 1; a < argc; ++a) {
@@ -80,6 +106,9 @@ int main(int argc, char** argv) {
     else if (k == "--accum") accum_path = v;
     else if (k == "--aperture") aperture = std::atof(v);
     else if (k == "--focus") focus = std::atof(v);
+    else if (k == "--devices") {
+      if (!parse_devices(v, devices)) return usage();
+    }
     else if (k == "--rows") {
       if (std::sscanf(v, "%d:%d", &row_off, &row_stride) != 2) return usage();
     } else return usage();
@@ -115,6 +144,10 @@ int main(int argc, char** argv) {
     world.add(make_shared<sphere>(point3(0, -100.5, 0), 100.0));
   } else if (scene == "book") {
     if (height < 0) height = (int)(width / 1.5);
+    if (!devices.empty()) {
+      std::cerr << "raytracer: --devices renders the reference integrator only\n";
+      return 2;
+    }
   } else if (scene == "final") {
     if (height < 0) height = (int)(width / 1.5);
     random_spheres(world, 1);
@@ -161,6 +194,8 @@ int main(int argc, char** argv) {
                   "rt_camera_look_at_lens");
       f = psrt::render_materials(sph, mats, lc, width, height, spp, depth, seed, row_off,
                                  row_stride);
+    } else if (!devices.empty()) {
+      f = psrt::render(world, cam, width, height, spp, depth, devices, seed, row_off, row_stride);
     } else {
       f = psrt::render(world, cam, width, height, spp, depth, seed, row_off, row_stride);
     }

@@ -161,7 +161,7 @@ struct Builder {
 
 }  // namespace
 
-BvhHost build_bvh(const rt_sphere* s, int n) {
+BvhHost build_bvh(const rt_sphere* s, int n, double big_ratio_in) {
   BvhHost out;
   if (n < kBvhMinSpheres || !s) return out;
   std::vector<double> radii;
@@ -176,8 +176,7 @@ BvhHost build_bvh(const rt_sphere* s, int n) {
   std::vector<double> sorted = radii;
   std::nth_element(sorted.begin(), sorted.begin() + n / 2, sorted.end());
   const double median = sorted[n / 2];
-  const char* er = std::getenv("PSRT_BIG_RATIO");  // tuning knob
-  const double big_ratio = er ? std::atof(er) : kBigRatio;
+  const double big_ratio = big_ratio_in > 0 ? big_ratio_in : kBigRatio;  // Tuning::big_ratio
   std::vector<Prim> prims;
   for (int i = 0; i < n; ++i) {
     if (radii[i] > big_ratio * median && radii[i] > 0) {

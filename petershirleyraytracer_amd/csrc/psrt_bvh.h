@@ -101,6 +101,8 @@ struct BvhHost {
 // Builds the structure; enabled = false when the scene is too small or
 // degenerate (non-finite or non-positive radii, huge coordinates), in which
 // case the device uses the linear sweep for every ray.
-BvhHost build_bvh(const rt_sphere* spheres, int n);
+// big_ratio: radius ratio (to the median) above which a sphere is tested on
+// every ray instead of entering the BVH; 0 = kBigRatio (rt_context_set_tuning)
+BvhHost build_bvh(const rt_sphere* spheres, int n, double big_ratio = 0);
 
 }  // namespace psrt

@@ -71,7 +71,7 @@ psrt::FastDiv fast_div_make(unsigned d) {
   return f;
 }
 
-// d_counters layout (words): [1, 5) totals (psrt_reduce), [8, 128) stamps
+// d_counters layout (words): [1, 1 + kStatWords) totals (psrt_reduce), [8, 128) stamps
 constexpr size_t kTotals = 1;
 constexpr size_t kHeads = 128;
 constexpr size_t kSets = kHeads + (size_t)psrt::kQueues * psrt::kShardStride;
@@ -81,14 +81,58 @@ constexpr size_t kCounterWords = kSets + (size_t)psrt::kQueues * psrt::kShardStr
 // free memory (rt_render_device)
 constexpr size_t kHbmReserve = (size_t)256 << 20;
 
-size_t sample_buffer_cap_bytes() {
-  const char* e = std::getenv("PSRT_SAMPLE_BUF_MB");
-  // default 48 GiB of the 288 GB HBM: C4 on one GPU (41 GB of sample
-  // records) in one chunk, C5 (96 GB) in 3; fewer chunks, fewer launch tails
-  // (measured: C4 564 -> 561 ms, C5 1312 -> 1306 ms against 16 GiB)
-  size_t mb = e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)49152;
-  if (mb < 1) mb = 1;
-  return mb << 20;
+}  // namespace
+
+namespace psrt {
+// Tuning knobs (rt_context_set_tuning; measurement and tests only). The
+// render path reads no environment variable: a context copies the process
+// defaults at creation, the one-shot entries' default contexts at each call.
+// Every knob keeps the output bit-identical.
+struct Tuning {
+  // sample-record buffer cap: 48 GiB of the 288 GB HBM holds C4 on one GPU
+  // (41 GB of records) in one chunk, C5 (96 GB) in 3; fewer chunks, fewer
+  // launch tails (measured: C4 564 -> 561 ms, C5 1312 -> 1306 ms against 16 GiB)
+  double sample_buf_mb = 49152;
+  double queue_k = 2, queue_d = 2;  // guided work queue shape (queue_phases)
+  double linear_chunk = 0;          // small-scene queue ticket (0: kLinearChunk)
+  double no_camlist = 0, no_neighbors = 0, no_fixpoint = 0, no_lds = 0;
+  double blocks_per_cu = 0;  // cap on resident trace workgroups per CU (0: occupancy max)
+  double mat_lds = -1;       // material kernel's scene in LDS: -1 auto, 0 off, 1 on
+  double mat_batch = 48;     // parked lanes per batched material walk (40-56 best, profiles/r03_mat)
+  double flush_at = 0;       // per-lane counter flush threshold (0: computed; tests force it low)
+  double stamps = 0;         // diagnostic kernel variant (section clocks, utilisation probes)
+  double scene_rebuild = 0;  // rebuild the culling structures for an unchanged scene
+  double big_ratio = 0;      // radius ratio of the big-sphere class (0: psrt_bvh's default)
+};
+}  // namespace psrt
+
+namespace {
+
+struct TuningKey {
+  const char* name;
+  double psrt::Tuning::*field;
+};
+const TuningKey kTuningKeys[] = {
+    {"sample_buf_mb", &psrt::Tuning::sample_buf_mb}, {"queue_k", &psrt::Tuning::queue_k},
+    {"queue_d", &psrt::Tuning::queue_d},             {"linear_chunk", &psrt::Tuning::linear_chunk},
+    {"no_camlist", &psrt::Tuning::no_camlist},       {"no_neighbors", &psrt::Tuning::no_neighbors},
+    {"no_fixpoint", &psrt::Tuning::no_fixpoint},     {"no_lds", &psrt::Tuning::no_lds},
+    {"blocks_per_cu", &psrt::Tuning::blocks_per_cu}, {"mat_lds", &psrt::Tuning::mat_lds},
+    {"mat_batch", &psrt::Tuning::mat_batch},         {"flush_at", &psrt::Tuning::flush_at},
+    {"stamps", &psrt::Tuning::stamps},               {"scene_rebuild", &psrt::Tuning::scene_rebuild},
+    {"big_ratio", &psrt::Tuning::big_ratio},
+};
+std::mutex g_tuning_mu;
+psrt::Tuning g_tuning;  // the process defaults (rt_context_set_tuning(NULL, ...))
+
+psrt::Tuning tuning_defaults() {
+  std::lock_guard<std::mutex> lk(g_tuning_mu);
+  return g_tuning;
+}
+
+size_t sample_buffer_cap_bytes(const psrt::Tuning& t) {
+  const double mb = t.sample_buf_mb >= 1 ? t.sample_buf_mb : 1;
+  return (size_t)mb << 20;
 }
 
 }  // namespace
@@ -152,7 +196,7 @@ struct rt_context {
   // pinned host memory: reading them back needs no copy kernel, which (like
   // any kernel) would wait for a free CU slot behind the next frame's
   // persistent trace launch
-  unsigned long long* h_stats = nullptr;  // [4] host pointer
+  unsigned long long* h_stats = nullptr;  // [kStatWords] host pointer
   unsigned long long* d_stats = nullptr;  // the same memory, device pointer
   std::vector<hipEvent_t> ev;  // pairs around each trace launch
   int ev_used = 0;
@@ -179,6 +223,8 @@ struct rt_context {
   bool last_mat = false;  // the last render used RT_FLAG_MATERIALS (no stamps to read)
   bool failed = false;    // the last render failed part-way (its timings are not reported)
   int fail_after = -1;    // rt_debug_fail_after_trace: the next render fails after this chunk
+  psrt::Tuning tune;      // rt_context_set_tuning
+  bool last_stamps = false;  // the last render ran the diagnostic variant (tune.stamps)
 };
 
 namespace {
@@ -235,9 +281,13 @@ rt_context* g_default[64] = {};
 // context: each holds that device's lock for the whole call.
 std::mutex g_device_mu[64];
 
+// RT_DEVICE (include/rt.h: the one-shot entries' device), read once
 int default_device() {
-  const char* e = std::getenv("RT_DEVICE");
-  return e ? std::atoi(e) : 0;
+  static const int dev = [] {
+    const char* e = std::getenv("RT_DEVICE");
+    return e ? std::atoi(e) : 0;
+  }();
+  return dev;
 }
 
 }  // namespace
@@ -276,6 +326,7 @@ int rt_context_create(int device, rt_context** out) {
   HIP_TRY(hipSetDevice(device));
   rt_context* c = new rt_context();
   c->device = device;
+  c->tune = tuning_defaults();
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, device));
   c->cus = prop.multiProcessorCount;
@@ -308,10 +359,10 @@ int rt_context_create(int device, rt_context** out) {
   // zeroed once: psrt_reduce leaves the queue heads and counter sets at zero
   HIP_TRY(hipMemsetAsync(c->d_counters, 0, kCounterWords * sizeof(unsigned long long), c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  HIP_TRY(hipHostMalloc((void**)&c->h_stats, 4 * sizeof(unsigned long long),
+  HIP_TRY(hipHostMalloc((void**)&c->h_stats, psrt::kStatWords * sizeof(unsigned long long),
                         hipHostMallocMapped | hipHostMallocCoherent));
   HIP_TRY(hipHostGetDevicePointer((void**)&c->d_stats, c->h_stats, 0));
-  std::fill(c->h_stats, c->h_stats + 4, 0ull);
+  std::fill(c->h_stats, c->h_stats + psrt::kStatWords, 0ull);
   HIP_TRY(hipEventCreate(&c->ev_all0));
   HIP_TRY(hipEventCreate(&c->ev_all1));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_plist, hipEventDisableTiming));
@@ -357,14 +408,16 @@ int rt_context_destroy(rt_context* c) {
 }
 
 // The FP32 pre-reject's sphere (psrt_kernels.hip test_sphere, Pre32): the
-// centre rounded to nearest and R = |r| + 2^-18 (|c|inf + |r|) + 2^-100
+// centre rounded to nearest and R = |r| + 2^-18 (|c|inf + |r|) + 2^-60
 // rounded up to FP32; +inf (never rejected) beyond 2^40 or for non-finite input.
 static float4 pre32_sphere(const rt_sphere& s) {
   const double ar = std::fabs(s.r);
   const double cm = std::max(std::fabs(s.cx), std::max(std::fabs(s.cy), std::fabs(s.cz)));
   float R = std::numeric_limits<float>::infinity();
   if (cm + ar <= 0x1p40) {  // false for NaN / inf
-    const double Rd = ar * (1.0 + 0x1p-18) + 0x1p-18 * cm + 0x1p-100;
+    // the floor 2^-60 keeps T*T >= 2^-120 a normal float, so its relative
+    // error bound holds at any scene scale (tests/host/pre32_check.c)
+    const double Rd = ar * (1.0 + 0x1p-18) + 0x1p-18 * cm + 0x1p-60;
     R = (float)Rd;
     if ((double)R < Rd) R = std::nextafter(R, std::numeric_limits<float>::infinity());
   }
@@ -383,7 +436,7 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
   // the culling structures, only the camera changes (its lists are rebuilt).
   if (n == c->n && n > 0 && (size_t)n == c->scene.size() &&
       std::memcmp(c->scene.data(), sph, (size_t)n * sizeof(rt_sphere)) == 0 &&
-      !std::getenv("PSRT_SCENE_REBUILD")) {
+      !c->tune.scene_rebuild) {
     c->cam = *cam;
     c->plist_valid = false;
     return RT_OK;
@@ -428,7 +481,7 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
   c->cam = *cam;
   c->plist_valid = false;
   // exact culling structure
-  const psrt::BvhHost b = psrt::build_bvh(sph, n);
+  const psrt::BvhHost b = psrt::build_bvh(sph, n, c->tune.big_ratio);
   (void)hipFree(c->d_nodes);
   (void)hipFree(c->d_leaf_geo);
   (void)hipFree(c->d_leaf_idx);
@@ -522,7 +575,7 @@ static psrt::BvhView bvh_view(const rt_context* c) {
   v.cell_rec = c->d_cell_rec;
   v.nb_rec = c->d_nb_rec;
   v.nb_c2 = 0.25 * c->pad * c->pad;
-  if (std::getenv("PSRT_NO_NEIGHBORS")) v.nb_c2 = -1.0;  // A/B knob: C^2 <= -r^2 never holds
+  if (c->tune.no_neighbors) v.nb_c2 = -1.0;  // C^2 <= -r^2 never holds
   // grid bounds / scale in FP32, as used: the cell index of the device is a
   // function of these exact float values, and the host places each sphere in
   // every cell its padded box overlaps under the SAME float cell boundaries
@@ -566,27 +619,25 @@ static int check_params(const rt_params* p) {
 // would outlast the rest of the launch. Working back from the end of the
 // queue, each later phase halves the size (down to 64) and holds about K
 // tickets per resident wave. Ticket ranges are contiguous: units a phase
-// cannot fill with whole tickets carry into the next one. PSRT_QUEUE_D /
-// PSRT_QUEUE_K: tuning knobs.
+// cannot fill with whole tickets carry into the next one. Tuning::queue_d /
+// queue_k: tuning knobs.
 // Small scenes (the linear sweep, ~5x cheaper rays) keep fixed tickets of
 // kLinearChunk units: there the queue's atomics and the per-wave start-up
 // cost more than the launch tail (C1: 0.31 ms with 1024-unit tickets on a few
 // hundred waves vs 0.51 ms guided; C2 -7% guided).
-static void queue_phases(psrt::TraceArgs& ta, int grid, bool guided) {
-  const char* ek = std::getenv("PSRT_QUEUE_K");
-  const char* ed = std::getenv("PSRT_QUEUE_D");
+static void queue_phases(psrt::TraceArgs& ta, int grid, bool guided, const psrt::Tuning& tu) {
   // two tickets per resident wave per phase (C3, 96 M units one frame at a
   // time: 13.64 -> 13.56 ms per step, r02), and the first ticket size at most
   // units / (2 x waves): the strong 1/8 shard's 20-frame launch (24 M units)
   // then starts with 1024-unit tickets instead of 512, and its trace takes
   // 1.480 instead of 1.503 ms per frame (r04, profiles/r04_queue; larger
   // launches are capped at 1024 either way)
-  const double k = ek ? std::atof(ek) : 2.0;
-  const double d = ed ? std::atof(ed) : 2.0;
+  const double k = tu.queue_k;
+  const double d = tu.queue_d;
   const uint64_t waves = (uint64_t)grid * (psrt::kTraceBlock / 64);
   unsigned s0 = guided ? psrt::kWorkChunk : psrt::kLinearChunk;
-  if (const char* el = std::getenv("PSRT_LINEAR_CHUNK"); el && !guided)  // tuning knob
-    s0 = std::max(64u, std::min(4096u, (unsigned)std::atoi(el)));
+  if (tu.linear_chunk > 0 && !guided)
+    s0 = std::max(64u, std::min(4096u, (unsigned)tu.linear_chunk));
   while (guided && s0 > 64 && (double)ta.total_units < d * (double)waves * (double)s0) s0 >>= 1;
   unsigned size[psrt::kQueuePhases];
   for (int p = 0; p < psrt::kQueuePhases; ++p) size[p] = guided ? std::max(64u, s0 >> p) : s0;
@@ -646,7 +697,7 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
   if (P == 0) {  // a shard that owns no rows: zero statistics, no launch
     const int qrc = quiesce(c);  // the last render's psrt_reduce writes h_stats
     if (qrc) return qrc;
-    std::fill(c->h_stats, c->h_stats + 4, 0ull);
+    std::fill(c->h_stats, c->h_stats + psrt::kStatWords, 0ull);
     HIP_TRY(hipEventRecord(c->ev_all0, st));
     HIP_TRY(hipEventRecord(c->ev_all1, st));
     c->in_flight = true;
@@ -669,23 +720,23 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
   if (s_units < 1) return set_error(RT_E_INVALID, "shard too large");
   // The buffer is sized to the HBM actually free: hipMemGetInfo's free bytes
   // plus this context's current buffer (it is replaced), less a reserve for
-  // the GPU's other users, capped by PSRT_SAMPLE_BUF_MB.
+  // the GPU's other users, capped by Tuning::sample_buf_mb.
   // The render's other buffers are decided first, so their growth comes out
   // of the same free HBM: the accumulator scratch (frames without a caller
   // accumulator, when the frame takes several chunks), the material path
   // scratch and the camera-ray lists.
   const bool use_bvh = c->bvh && !(p->flags & RT_FLAG_NO_CULL);
   // material kernel: the BVH staged in LDS when the workgroups resident per CU
-  // stay as many as without (PSRT_MAT_LDS=0/1 forces it off / on)
+  // stay as many as without (Tuning::mat_lds 0 / 1 forces it off / on)
   int mat_grid = use_bvh ? c->grid_mat_bvh : c->grid_mat;
   unsigned mat_lds = 0;
   if (mat && use_bvh) {
     const unsigned bytes = psrt::mat_lds_layout(c->n, c->n_nodes, c->n_leaf, c->n_big).bytes;
     int pc = 0;
-    const char* ml = std::getenv("PSRT_MAT_LDS");
+    const double ml = c->tune.mat_lds;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, psrt::psrt_trace_mat<true, true, false>,
                                                      psrt::kMatBlock, bytes) == hipSuccess &&
-        pc >= 1 && (ml ? std::atoi(ml) != 0 : c->cus * pc >= c->grid_mat_bvh)) {
+        pc >= 1 && (ml >= 0 ? ml != 0 : c->cus * pc >= c->grid_mat_bvh)) {
       mat_lds = bytes;
       mat_grid = c->cus * pc;
     }
@@ -697,14 +748,14 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
   const double om = std::max(std::fabs(c->cam.origin[0]),
                              std::max(std::fabs(c->cam.origin[1]), std::fabs(c->cam.origin[2])));
   const bool camlist = !mat && use_bvh && c->n < (int)psrt::kCamOverflow && om <= c->r_check &&
-                       !std::getenv("PSRT_NO_CAMLIST");
+                       !c->tune.no_camlist;
   // the material integrator's lists through the lens: the same conditions,
   // for the lens camera's origin
   const double lom = std::max(std::fabs(c->lcam.base.origin[0]),
                               std::max(std::fabs(c->lcam.base.origin[1]),
                                        std::fabs(c->lcam.base.origin[2])));
   const bool mat_list = mat && use_bvh && c->n < (int)psrt::kCamOverflow && lom <= c->r_check &&
-                        !std::getenv("PSRT_NO_CAMLIST");
+                        !c->tune.no_camlist;
   bool any_null_acc = false;
   for (size_t f = 0; f < nf; ++f) any_null_acc = any_null_acc || !(d_accum_f && d_accum_f[f]);
   auto grow = [](size_t need, size_t have, size_t unit) { return need > have ? (need - have) * unit : 0; };
@@ -712,7 +763,7 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
                              grow(path_ints, c->path_cap, sizeof(int)) +
                              (camlist ? grow(P, c->plist_cap, sizeof(uint4)) : 0) +
                              (mat_list ? grow(P, c->mat_plist_cap, sizeof(uint4)) : 0);
-  size_t cap_bytes = sample_buffer_cap_bytes();
+  size_t cap_bytes = sample_buffer_cap_bytes(c->tune);
   // the current buffer already holds the whole render in one chunk: no query
   // (hipMemGetInfo is a host round trip on every render otherwise)
   const size_t recs_all = nf * P * (size_t)p->spp;
@@ -814,8 +865,7 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     ma.mats = c->d_mats;
     ma.path = c->d_path;
     ma.path_stride = (unsigned)lanes;
-    const char* mb = std::getenv("PSRT_MAT_BATCH");  // tuning knob
-    ma.batch = mb ? (unsigned)std::max(1, std::atoi(mb)) : 48u;  // 40-56 best (profiles/r03_mat)
+    ma.batch = (unsigned)std::max(1.0, c->tune.mat_batch);
   }
 
   psrt::TraceArgs ta{};
@@ -843,7 +893,7 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
   // No memset here: the queue heads and counter sets are zero (context
   // creation, then every psrt_reduce), and a small fill kernel on this stream
   // would wait for a CU slot behind another frame's persistent launch.
-  const bool stamps = !mat && std::getenv("PSRT_STAMPS") != nullptr;  // diagnostic build
+  const bool stamps = !mat && c->tune.stamps != 0;  // the diagnostic variant
   if (stamps) HIP_TRY(hipMemsetAsync(c->d_counters + 8, 0, 120 * sizeof(unsigned long long), st));
   ta.stamps = c->d_counters + 8;
   ta.wave_log = nullptr;
@@ -871,17 +921,15 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     // `rays` is always exact), <= (max_depth + 1)(4n + 16) sphere / box tests
     // (hint + big + list <= 2n + 16, leaves <= n; box tests <= 2 per node).
     // flush_at leaves that much headroom below 2^32 (the test counts stay exact
-    // while one sample's tests are < 2^32). PSRT_FLUSH_AT: test knob, >= 1.
+    // while one sample's tests are < 2^32). Tuning::flush_at: test knob, >= 1.
     const uint64_t per_sample = (uint64_t)(p->max_depth + 1) * (4ull * (uint64_t)c->n + 16ull);
     const uint64_t room = per_sample < 0xFFFFFFFFull ? 0xFFFFFFFFull - per_sample : 1ull;
     ta.flush_at = (unsigned)std::max<uint64_t>(1ull, std::min<uint64_t>(room, 0x80000000ull));
-    if (const char* fa = std::getenv("PSRT_FLUSH_AT")) {
-      const unsigned long v = std::strtoul(fa, nullptr, 10);
-      if (v >= 1 && v < ta.flush_at) ta.flush_at = (unsigned)v;
-    }
+    if (c->tune.flush_at >= 1 && c->tune.flush_at < ta.flush_at)
+      ta.flush_at = (unsigned)c->tune.flush_at;
   }
   psrt::BvhView bv = bvh_view(c);
-  bv.fixpoint = !(p->flags & RT_FLAG_NO_FIXPOINT) && !std::getenv("PSRT_NO_FIXPOINT");
+  bv.fixpoint = !(p->flags & RT_FLAG_NO_FIXPOINT) && !c->tune.no_fixpoint;
   if (mat_list && c->mat_plist_cap < P) {
     rc = quiesce(c);
     if (rc) return rc;
@@ -1011,6 +1059,8 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
                : mlaunch(psrt::psrt_trace_mat<false, false, false>, 0);
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipEventRecord(c->ev[2 * ch + 1], st));
+      if (ch == fail_at)
+        return set_error(RT_E_HIP, "rt_debug_fail_after_trace: failure injected after chunk %d", ch);
       for (size_t f = 0; f < nf; ++f) {
         psrt::ReduceArgs ra{};
         ra.samp_t = c->d_samples + 3 * f * fu;
@@ -1032,7 +1082,7 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
       }
       continue;
     }
-    queue_phases(ta, use_bvh ? c->grid_bvh : c->grid, use_bvh);
+    queue_phases(ta, use_bvh ? c->grid_bvh : c->grid, use_bvh, c->tune);
     HIP_TRY(hipEventRecord(c->ev[2 * ch], st));
     const double4* g4 = c->d_geo;
     const double* ir = c->d_inv_r;
@@ -1040,11 +1090,11 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     // scene data in LDS when three workgroups per CU still fit (the BVH
     // kernel's resident count otherwise: its global-memory variant)
     const unsigned lds_bytes = psrt::lds_layout(c->n, c->n_nodes, c->n_leaf, c->n_big).bytes;
-    const bool lds = use_bvh && lds_bytes <= c->lds_max && !std::getenv("PSRT_NO_LDS");
-    // PSRT_BLOCKS_PER_CU: measurement knob (occupancy sweep), default = resident max
-    const char* bpc = std::getenv("PSRT_BLOCKS_PER_CU");
+    const bool lds = use_bvh && lds_bytes <= c->lds_max && !c->tune.no_lds;
+    // Tuning::blocks_per_cu: measurement knob (occupancy sweep), 0 = resident max
+    const int bpc = (int)c->tune.blocks_per_cu;
     auto launch = [&](auto kern, int grid) {
-      if (bpc) grid = std::min(grid, std::max(1, c->cus * std::atoi(bpc)));
+      if (bpc > 0) grid = std::min(grid, std::max(1, c->cus * bpc));
       hipLaunchKernelGGL(kern, dim3(grid), blk, lds ? lds_bytes : 0, st, g4, ir, c->d_samples, ta,
                          bv);
     };
@@ -1092,7 +1142,12 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     size_t acc_stride = 0, rgb_stride = 0;
     std::vector<unsigned char*> rgb_now(nf, nullptr);
     for (size_t f = 0; f < nf; ++f) rgb_now[f] = last ? rgb[f] : nullptr;
-    const bool one = strided(acc.data(), acc_stride) && strided(rgb_now.data(), rgb_stride);
+    // one launch reduces the frames concurrently: only when no two frames'
+    // buffers overlap (a stride of at least one frame); overlapping buffers
+    // keep the per-frame launches, in frame order
+    const bool one = strided(acc.data(), acc_stride) && strided(rgb_now.data(), rgb_stride) &&
+                     (nf == 1 || ((acc_stride == 0 || acc_stride >= 3 * P) &&
+                                  (rgb_stride == 0 || rgb_stride >= 3 * P)));
     for (size_t f0 = 0; f0 < nf; f0 += one ? nf : 1) {
       psrt::ReduceArgs ra{};
       ra.samp_t = c->d_samples + f0 * fu;
@@ -1126,6 +1181,7 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
   c->in_flight = fence == hipSuccess;
   c->last_stream = st;
   c->last_mat = mat;
+  c->last_stamps = stamps;
   if (rc) {
     // a failed render's timings are not reported: no event pair is summed
     // (kernel_ms and total_ms read 0 until the next successful render)
@@ -1161,8 +1217,8 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
     return RT_OK;
   }
   // the render's last psrt_reduce wrote its totals into pinned host memory
-  unsigned long long cnt[4];
-  for (int k = 0; k < 4; ++k) cnt[k] = ((volatile unsigned long long*)c->h_stats)[k];
+  unsigned long long cnt[psrt::kStatWords];
+  for (int k = 0; k < psrt::kStatWords; ++k) cnt[k] = ((volatile unsigned long long*)c->h_stats)[k];
   const unsigned long long rays = cnt[0];
   double kms = 0.0;
   for (int ch = 0; ch < c->ev_used; ++ch) {
@@ -1177,9 +1233,11 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   c->last.tests_executed = cnt[1];
   c->last.box_tests = cnt[2];
   c->last.rays_traced = cnt[3];
+  c->last.prerejects = cnt[4];
+  c->last.root_box_tests = cnt[5];
   c->last.kernel_ms = kms;
   c->last.total_ms = all;
-  if (std::getenv("PSRT_STAMPS") && !c->last_mat) {
+  if (c->last_stamps) {  // the diagnostic variant's section clocks and probes
     unsigned long long sec[60];
     HIP_TRY(hipMemcpy(sec, c->d_counters + 8, sizeof sec, hipMemcpyDeviceToHost));
     static const char* names[24] = {"refill", "store", "hit", "hint", "nb", "cam",
@@ -1280,6 +1338,7 @@ static int get_default_context(rt_context** out, std::unique_lock<std::mutex>* l
     if (rc) return rc;
   }
   *out = g_default[dev];
+  (*out)->tune = tuning_defaults();  // the process defaults at each one-shot call
   return RT_OK;
 }
 
@@ -1400,6 +1459,34 @@ int rt_debug_fail_after_trace(rt_context* c, int chunk) {
   if (!c) return set_error(RT_E_INVALID, "rt_debug_fail_after_trace: ctx is NULL");
   c->fail_after = chunk < 0 ? -1 : chunk;
   return RT_OK;
+}
+
+int rt_context_set_tuning(rt_context* c, const char* name, double value) {
+  if (!name) return set_error(RT_E_INVALID, "rt_context_set_tuning: name is NULL");
+  for (const TuningKey& k : kTuningKeys) {
+    if (std::strcmp(k.name, name) != 0) continue;
+    if (!std::isfinite(value))
+      return set_error(RT_E_INVALID, "rt_context_set_tuning: %s must be finite", name);
+    if (c) {
+      c->tune.*k.field = value;
+    } else {
+      std::lock_guard<std::mutex> lk(g_tuning_mu);
+      g_tuning.*k.field = value;
+    }
+    return RT_OK;
+  }
+  return set_error(RT_E_INVALID, "rt_context_set_tuning: unknown knob '%s'", name);
+}
+
+int rt_context_get_tuning(rt_context* c, const char* name, double* value) {
+  if (!name || !value) return set_error(RT_E_INVALID, "rt_context_get_tuning: bad arguments");
+  const psrt::Tuning t = c ? c->tune : tuning_defaults();
+  for (const TuningKey& k : kTuningKeys) {
+    if (std::strcmp(k.name, name) != 0) continue;
+    *value = t.*k.field;
+    return RT_OK;
+  }
+  return set_error(RT_E_INVALID, "rt_context_get_tuning: unknown knob '%s'", name);
 }
 
 int rt_debug_probe_f64(int op, const double* x, const double* y, double* out, int n) {

@@ -28,6 +28,10 @@ constexpr int kQueuePhases = 5;        // guided: ticket sizes halve toward the 
 // the end of the work moves on to the next heads (stealing) before it stops.
 constexpr int kQueues = PSRT_QUEUES;
 constexpr int kShardStride = 16;       // u64 words between heads / counter sets (128 B)
+// Statistics words of a counter set / the render's totals: [0] rays, [1] full
+// FP64 sphere tests, [2] FP32 box tests, [3] traced rays, [4] FP32 sphere
+// pre-rejects, [5] FP64 root-box tests ([1], [2], [4], [5]: counting variant only)
+constexpr int kStatWords = 6;
 // Scene data psrt_trace stages in (dynamic) LDS per workgroup: BVH nodes (2
 // float4 each, plus the padding node), spheres {c, r*r}, 1/r, leaf slots and
 // neighbour records (8 B), FP32 pre-reject spheres and the big-sphere
@@ -72,9 +76,6 @@ constexpr int kReduceBlock = 64;   // psrt_reduce: one wave per 64 pixels
 #define PSRT_REDUCE_IN_FLIGHT 2
 #endif
 constexpr unsigned kReduceInFlight = PSRT_REDUCE_IN_FLIGHT;  // psrt_reduce: sample tiles in flight per wave
-#ifndef PSRT_REDUCE_NT
-#define PSRT_REDUCE_NT 0  // psrt_reduce: non-temporal sample loads (A/B knob)
-#endif
 #ifndef PSRT_REDUCE_TILE
 #define PSRT_REDUCE_TILE 32
 #endif
@@ -105,8 +106,8 @@ struct TraceArgs {
   uint64_t ph_first[kQueuePhases + 1];
   uint64_t ph_base[kQueuePhases];
   unsigned ph_size[kQueuePhases];
-  unsigned long long* ray_counter;  // kQueues sets, kShardStride apart: [0] rays, [1] sphere
-                                    // tests, [2] box tests, [3] traced rays (host sums them)
+  unsigned long long* ray_counter;  // kQueues sets, kShardStride apart: kStatWords counters
+                                    // (rays, tests by kind, traced rays; psrt_reduce sums them)
   unsigned long long* stamps;       // diagnostic build: cycles per section (kSecCount)
   unsigned long long* wave_log;     // diagnostic build: per wave {start, queue empty, exit,
                                     // iterations at queue empty, at exit} (s_memrealtime,
@@ -154,7 +155,7 @@ struct BvhView {
   const uint4* __restrict__ cell_rec;  // [2 * ncell]
   const uint2* __restrict__ nb_rec;    // [n]
   // per sphere {fl(cx), fl(cy), fl(cz), R}, R >= |r| + 2^-18 (|c|inf + |r|) +
-  // 2^-100 rounded up (+inf beyond 2^40): the FP32 pre-reject (psrt_kernels.hip
+  // 2^-60 rounded up (+inf beyond 2^40): the FP32 pre-reject (psrt_kernels.hip
   // Pre32) of test_sphere
   const float4* __restrict__ geo32;    // [n]
 };
@@ -201,8 +202,8 @@ struct ReduceArgs {
   // the last chunk also writes totals to host_stats (pinned host memory).
   unsigned long long* heads;       // TraceArgs::work_counter (kQueues heads)
   unsigned long long* sets;        // TraceArgs::ray_counter (kQueues sets)
-  unsigned long long* totals;      // [4], device
-  unsigned long long* host_stats;  // [4], or nullptr
+  unsigned long long* totals;      // [kStatWords], device
+  unsigned long long* host_stats;  // [kStatWords], or nullptr
 };
 
 // ---- material integrator (psrt_mat.hip) ----

@@ -66,17 +66,17 @@ constexpr int kRngExtra = PSRT_RNG_EXTRA;  // extra trials while a scattering la
 
 __device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
 
-// Section ablation (measurement builds only, PSRT_ABLATE = section id): the
-// section runs a second time on copies of its state, the copy's results sunk
-// here, so PMC SQ_INSTS_VALU and the kernel time grow by that section's cost
-// (DESIGN.md §4 census). The default build has PSRT_ABLATE = 0.
+// Section ablation for the census: measurement builds only
+// (PSRT_ABLATE = section id, psrt_ablate.h); in the product build every
+// PSRT_ABLATE_AT hook is empty.
 #ifndef PSRT_ABLATE
 #define PSRT_ABLATE 0
 #endif
-template <class T>
-__device__ __forceinline__ void ablate_sink(T v) {
-  asm volatile("" ::"v"(v));
-}
+#if PSRT_ABLATE
+#include "psrt_ablate.h"
+#else
+#define PSRT_ABLATE_AT(site)
+#endif
 
 // Diagnostic build only (kStamps): wave-level cycle accounting per kernel
 // section, one s_memtime per boundary (cdna_hip_programming.md §7 stamps).
@@ -306,7 +306,8 @@ __device__ __forceinline__ int sweep_linear(const double4* __restrict__ geo, int
 // HALF_B^2). With o, c and A in range (below), let a = fl(fl(o) - fl(c)) per
 // axis, L = fl(ax^2 + ay^2 + az^2) (two FMAs) and T = fl(fl(bt) sk +
 // fl(mo + R)), where sk >= sqrt(A) (1 + 2^-17), mo >= 2^-18 |o|inf and
-// R >= |r| + 2^-18 (|c|inf + |r|) + 2^-100 (host, rounded up). Rounding
+// R >= |r| + 2^-18 (|c|inf + |r|) + 2^-60 (host, rounded up; the floor keeps
+// T^2 >= 2^-120 a normal float). Rounding
 // analysis (u = 2^-24): |a - amc| <= 3.5u (|o|inf + |c|inf), L <= |a|^2
 // (1 + 3.01u), fl(T T) >= T^2 (1 - u), so L > fl(T T) gives
 // D > bt sqrt(A) (1 + 2^-18.1) + 2^-18.1 (|o|inf + |c|inf + |r|) >= bt sqrt(A)
@@ -317,7 +318,8 @@ __device__ __forceinline__ int sweep_linear(const double4* __restrict__ geo, int
 // ~20 FP64 ones (4 cycles each); its margin (2^-18 relative) rejects at the
 // distances the FP64 one did (D >= 2^-17 |amc|). C3 psrt_trace 12.08 ->
 // 11.80 ms (profiles/r04_pre32/ab.txt); tests/host/pre32_check.c checks it
-// against the reference test on 4 M adversarial cases.
+// against the reference test on 8.2 M adversarial cases, at scene scales
+// from 1 down to 2^-90.
 // Returns false when the pre-reject decided the sphere, true when the full
 // test ran. *c_out (if given) receives C = amc.amc - r^2 as sphere.cc:11 forms it.
 struct Pre32 {
@@ -376,9 +378,18 @@ struct NullCount {
   __device__ NullCount& operator++() { return *this; }
   __device__ operator unsigned() const { return 0u; }
 };
+// What the counting variant tallies, by the kind of test that actually ran
+// (bench.py weights each kind by its measured issue cost):
+//   fp64   sphere tests run in full in FP64 (sphere.cc:6-31; the hint test,
+//          big / listed / leaf spheres past the pre-reject, the linear sweep)
+//   pre    sphere candidates decided by the FP32 pre-reject (Pre32) alone
+//   boxes  FP32 slab tests evaluated in the BVH walk (node + 1's test only
+//          when it ran)
+//   root   FP64 root-box tests (far origins, hit_quick)
+// Candidates skipped because they are the hint sphere count as nothing.
 template <bool kCount>
 struct CullStatsT {
-  std::conditional_t<kCount, unsigned, NullCount> boxes, spheres;
+  std::conditional_t<kCount, unsigned, NullCount> boxes, fp64, pre, root;
   // diagnostic build only: wave-level loop trips (counted by the first
   // active lane) vs lane-level work, to measure traversal divergence
   unsigned wave_trips = 0, wave_leaf_trips = 0, trav_rays = 0, leaf_visits = 0;
@@ -448,7 +459,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
   const double am = __builtin_fmax(__builtin_fabs(ox),
                                    __builtin_fmax(__builtin_fabs(oy), __builtin_fabs(oz)));
   if (!finite || !(am < 1e200)) {  // unbounded arithmetic: the reference scan, verbatim
-    cs.spheres += n;
+    cs.fp64 += n;
     bi = sweep_linear(geo, n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), bt);
     return true;
   }
@@ -466,16 +477,9 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     double ch;
     // the ray's first test: bt = +inf, so no pre-reject
     test_sphere<false>(sh, hint, ox, oy, oz, dx, dy, dz, A, bt, bi, float4{}, pr, &ch);
-#if PSRT_ABLATE == 6
-    {
-      double bt2 = __builtin_inf(), ch2;
-      int bi2 = -1;
-      test_sphere<false>(sh, hint, ox, oy, oz, dx, dy, dz, A, bt2, bi2, float4{}, pr, &ch2);
-      ablate_sink(bt2), ablate_sink(bi2), ablate_sink(ch2);
-    }
-#endif
+    PSRT_ABLATE_AT(HINT);
     fix = bv.fixpoint && ch == 0.0 && sh.w >= 0x1p-700 && sh.w <= 0x1p700 && am <= 0x1p40;
-    ++cs.spheres;
+    ++cs.fp64;
     if (bi == hint) {
       clk.util(kUHintHit);
       if (bt < 1e-6) clk.util(kUHintTiny);
@@ -494,27 +498,18 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     }
   }
   clk.mark(kSecQHint);
-#if PSRT_ABLATE == 7
-  {
-    double bt2 = bt;
-    int bi2 = bi;
-    bool f2 = false;
-    for (int b = 0; b < bv.n_big; ++b) {
-      const int idx = lbig[b];
-      if (idx != hint)
-        f2 |= test_sphere(sv.geo(idx), idx, ox, oy, oz, dx, dy, dz, A, bt2, bi2, sv.g32(idx), pr);
-    }
-    ablate_sink(bt2), ablate_sink(bi2), ablate_sink(f2);
-  }
-#endif
+  PSRT_ABLATE_AT(BIG);
   // the big spheres from the scene copy in LDS (kLds; the global arrays
   // otherwise): their indices, spheres and FP32 spheres
   for (int b = 0; b < bv.n_big; ++b) {
     const int idx = lbig[b];
-    if (idx != hint)
-      full |= test_sphere(sv.geo(idx), idx, ox, oy, oz, dx, dy, dz, A, bt, bi, sv.g32(idx), pr);
+    if (idx != hint) {
+      const bool ran = test_sphere(sv.geo(idx), idx, ox, oy, oz, dx, dy, dz, A, bt, bi, sv.g32(idx), pr);
+      full |= ran;
+      cs.fp64 += ran;
+      cs.pre += !ran;
+    }
   }
-  cs.spheres += bv.n_big;
   clk.mark(kSecQBig);
   // The candidate list of this ray, one of:
   //   neighbour list of the hint sphere (nb path), the pixel's camera list,
@@ -552,31 +547,18 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
   }
   const int cnt = listed ? (int)(rec.x & 0xFFFFu) : 0;
   uint64_t lo = rec.x | (uint64_t)rec.y << 32, hi = rec.z | (uint64_t)rec.w << 32;
-#if PSRT_ABLATE == 8
-  {
-    double bt2 = bt;
-    int bi2 = bi;
-    bool f2 = false;
-    uint64_t lo2 = lo, hi2 = hi;
-    for (int e = 0; e < cnt; ++e) {
-      lo2 = (lo2 >> 16) | (hi2 << 48);
-      hi2 >>= 16;
-      const int idx = (int)(lo2 & 0xFFFFu);
-      if (idx == hint) continue;
-      f2 |= test_sphere(sv.geo(idx), idx, ox, oy, oz, dx, dy, dz, A, bt2, bi2, sv.g32(idx), pr);
-    }
-    ablate_sink(bt2), ablate_sink(bi2), ablate_sink(f2);
-  }
-#endif
+  PSRT_ABLATE_AT(LIST);
   for (int e = 0; e < cnt; ++e) {
     clk.util(kUListTrip);
     lo = (lo >> 16) | (hi << 48);
     hi >>= 16;
     const int idx = (int)(lo & 0xFFFFu);
     if (idx == hint) continue;
-    full |= test_sphere(sv.geo(idx), idx, ox, oy, oz, dx, dy, dz, A, bt, bi, sv.g32(idx), pr);
+    const bool ran = test_sphere(sv.geo(idx), idx, ox, oy, oz, dx, dy, dz, A, bt, bi, sv.g32(idx), pr);
+    full |= ran;
+    cs.fp64 += ran;
+    cs.pre += !ran;
   }
-  cs.spheres += cnt;
   clk.mark(kSecQGrid);
   if (listed) {
     trapped = fix && !full && bi == hint;
@@ -587,15 +569,18 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     // padded root box in FP64 (error ~1e-13 relative, far inside the pad). A
     // miss proves no BVH sphere can have a root in [0, bt]; a hit parks the
     // ray for the batched walk, which re-bases it at the box entry (hit_traverse).
-    ++cs.boxes;
+    ++cs.root;
     const double e = root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt);
     if (e < 0.0) {
       clk.util(kUFarMiss);
       return true;
     }
-    // the walk re-bases the ray here (hit_traverse); any nearby point of the
-    // ray serves, so the float rounding of the entry is harmless
-    t0f = (float)e;
+    // The walk re-bases the ray here (hit_traverse). Any nearby point of the
+    // ray serves while the float rounding of e moves it by <= 2^-24 e |d| <=
+    // r_check / 4 (then |o'| stays in the range the slab test's error bound
+    // covers, psrt_bvh.cpp); an origin farther out than that (a camera
+    // ~2^22 r_check away) gets -1: the walk recomputes the entry in FP64.
+    t0f = (e * e) * A <= gc.rebase_lim ? (float)e : -1.0f;
   }
   clk.util(kUPark);
   return false;
@@ -611,6 +596,19 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
                                              double ox, double oy, double oz, double dx, double dy,
                                              double dz, double A, double& bt, int& bi,
                                              CS& cs, int& node, unsigned tail, double t0) {
+  // t0 < 0: an origin too far out for a float entry (hit_quick): the entry
+  // in FP64, for the current bt; a segment that now misses the root box
+  // (bt shrank in an earlier pass) can improve on nothing: the walk is over
+  if (__builtin_expect(__ballot(t0 < 0.0) != 0, 0)) {
+    if (t0 < 0.0) {
+      ++cs.root;
+      t0 = root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt);
+      if (t0 < 0.0) {
+        t0 = 0.0;
+        node = bv.n_nodes;
+      }
+    }
+  }
   // Far origins are re-based at their root-box entry o' = o + t0 d (FP64), so
   // the FP32 slab test sees |o'| <= the scene scale and its error bound holds;
   // box intervals are then tested over [-t0, bt - t0]. The exact sphere tests
@@ -668,7 +666,7 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
       } else {
         next = node + 2;
       }
-      cs.boxes += 2;
+      cs.boxes += 1u + (hit_a && leaf_a < 0);  // node + 1 was tested only after an interior hit
       node = next;
     }
     if (leaf >= 0) {
@@ -681,9 +679,10 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
       for (int k = first; k < first + cnt; ++k) {
         const int idx = leaf_idx[k];
         if (idx == hint) continue;
-        test_sphere(kLdsLeaves ? sv.geo(idx) : bv.leaf_geo[k], idx, ox, oy, oz, dx, dy, dz, A, bt,
-                    bi, sv.g32(idx), pr);
-        ++cs.spheres;
+        const bool ran = test_sphere(kLdsLeaves ? sv.geo(idx) : bv.leaf_geo[k], idx, ox, oy, oz,
+                                     dx, dy, dz, A, bt, bi, sv.g32(idx), pr);
+        cs.fp64 += ran;
+        cs.pre += !ran;
       }
       tmax = tmax_up(bt - t0);
       leaf = -1;
@@ -715,20 +714,22 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
 }
 
 
-// rays / sphere tests / box tests of this wave (32-bit per lane) -> one 64-bit
-// atomic each. Called converged (whole wave).
+// A wave's per-lane 32-bit counters -> one 64-bit atomic each into the
+// block's counter set (psrt_kernels.h TraceArgs::ray_counter: [0] rays,
+// [1] full FP64 sphere tests, [2] box tests, [4] pre-rejects, [5] root-box
+// tests). Called converged (whole wave).
+template <bool kCount>
 __device__ __forceinline__ void flush_counters(unsigned long long* ctr, unsigned rays,
-                                            unsigned spheres, unsigned boxes, unsigned lane) {
-  unsigned long long wr = rays, ws = spheres, wb = boxes;
-  for (int off = 32; off > 0; off >>= 1) {
-    wr += __shfl_xor(wr, off);
-    ws += __shfl_xor(ws, off);
-    wb += __shfl_xor(wb, off);
-  }
-  if (lane == 0) {
-    if (wr) atomicAdd(ctr, wr);
-    if (ws) atomicAdd(ctr + 1, ws);
-    if (wb) atomicAdd(ctr + 2, wb);
+                                               const CullStatsT<kCount>& cs, unsigned lane) {
+  constexpr int kN = kCount ? 5 : 3;
+  const unsigned v[5] = {rays, (unsigned)cs.fp64, (unsigned)cs.boxes, (unsigned)cs.pre,
+                         (unsigned)cs.root};
+  constexpr int slot[5] = {0, 1, 2, 4, 5};
+#pragma unroll
+  for (int c = 0; c < kN; ++c) {
+    unsigned long long w = v[c];
+    for (int off = 32; off > 0; off >>= 1) w += __shfl_xor(w, off);
+    if (lane == 0 && w) atomicAdd(ctr + slot[c], w);
   }
 }
 
@@ -757,8 +758,11 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
   // the loop they would take ~40 registers and spill to scratch.
   __shared__ RefillConst s_rc;
   __shared__ GridC s_gc;
-  __shared__ unsigned long long s_flush[3];  // counters flushed from the lanes (refill block)
-  if (threadIdx.x < 3) s_flush[threadIdx.x] = 0ull;
+  // counters flushed from the lanes (refill block): rays, then (counting
+  // variant) the tests by kind, in the counter-set order
+  constexpr unsigned kFlushWords = kCount ? 6 : 3;
+  __shared__ unsigned long long s_flush[kFlushWords];
+  if (threadIdx.x < kFlushWords) s_flush[threadIdx.x] = 0ull;
   if (threadIdx.x == 0) s_gc = grid_consts(bv);
   if (threadIdx.x < 12)
     s_rc.cam[threadIdx.x] = threadIdx.x < 3   ? a.org[threadIdx.x]
@@ -831,7 +835,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
   bool qv0 = false, qv1 = false;  // slot 0 / slot 1 of the queue hold a trial
   double pbt = 0.0;      // closest t / index so far of this ray's world.hit
   int pbi = -1;
-  CullStatsT<kCount> cs{0u, 0u};
+  CullStatsT<kCount> cs{};
   unsigned long long traced = 0;  // wave-uniform: rays this wave traced
   SectionClock<kStamps> clk;
   __shared__ unsigned s_util[kStamps ? 2 * kUCount : 1];
@@ -865,11 +869,18 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
       // adds at most one sample's work (it idles once its sample ends), which the
       // host bounds below 2^32 - a.flush_at: flush them to the 64-bit totals
       // once any lane's reaches a.flush_at (tests set it low to run this path).
-      if (__builtin_expect(__ballot(max(rays, max((unsigned)cs.spheres, (unsigned)cs.boxes)) >= a.flush_at) != 0, 0)) {
+      if (__builtin_expect(__ballot(max(rays, max(max((unsigned)cs.fp64, (unsigned)cs.boxes),
+                                                  max((unsigned)cs.pre, (unsigned)cs.root))) >=
+                                    a.flush_at) != 0, 0)) {
         atomicAdd(&s_flush[0], (unsigned long long)rays);  // LDS; to HBM at exit
-        atomicAdd(&s_flush[1], (unsigned long long)cs.spheres);
+        atomicAdd(&s_flush[1], (unsigned long long)cs.fp64);
         atomicAdd(&s_flush[2], (unsigned long long)cs.boxes);
-        rays = cs.spheres = cs.boxes = 0u;
+        if constexpr (kCount) {
+          atomicAdd(&s_flush[4], (unsigned long long)cs.pre);
+          atomicAdd(&s_flush[5], (unsigned long long)cs.root);
+        }
+        rays = 0u;
+        cs.fp64 = cs.boxes = cs.pre = cs.root = 0u;
       }
       // sky (main.cc:46-48) x 0.5^k, or black; store
       [[maybe_unused]] const bool stored = done;
@@ -940,18 +951,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
           const int j = rc.hm1_i - r;
           const unsigned pix = (unsigned)j * dw.d + i;
           const unsigned s = (unsigned)rc.s_begin + sl;
-#if PSRT_ABLATE == 5
-          {
-            uint64_t r2 = splitmix64((((uint64_t)pix) << 32 | (uint64_t)s) ^ rc.seedmix[f]);
-            const double xu2 = (double)i + random_double(r2), xv2 = (double)j + random_double(r2);
-            const double u2 = div_by(xu2, rc.wm1, rc.rwm1), v2 = div_by(xv2, rc.hm1, rc.rhm1);
-            const double* c2 = rc.cam;
-            const double ex = ((c2[3] + u2 * c2[6]) + v2 * c2[9]) - c2[0];
-            const double ey = ((c2[4] + u2 * c2[7]) + v2 * c2[10]) - c2[1];
-            const double ez = ((c2[5] + u2 * c2[8]) + v2 * c2[11]) - c2[2];
-            ablate_sink((ex * ex + ey * ey) + ez * ez), ablate_sink(r2);
-          }
-#endif
+          PSRT_ABLATE_AT(REFILL);
           rng = splitmix64((((uint64_t)pix) << 32 | (uint64_t)s) ^ rc.seedmix[f]);
           // main.cc:80-81, camera.h:25-28
           const double xu = (double)i + random_double(rng);
@@ -1023,18 +1023,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
           const GridC& gc = *(const GridC*)((const char*)&s_gc + zg);
           resolved = hit_quick(geo, sv, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, pbt, pbi,
                                cs, clk, trapped, q, gc, lbig, wt0);
-#if PSRT_ABLATE == 1
-          {
-            double bt2;
-            int bi2;
-            bool tr2;
-            CullStatsT<false> cs2{0u, 0u};
-            float t02;
-            const bool r2 = hit_quick(geo, sv, a.n, bv, hint, ox, oy, oz, dx, dy, dz, A, bt2,
-                                      bi2, cs2, clk, tr2, q, gc, lbig, t02);
-            ablate_sink(bt2), ablate_sink(bi2), ablate_sink(tr2), ablate_sink(r2);
-          }
-#endif
+          PSRT_ABLATE_AT(HIT_QUICK);
           pending = !resolved;
           wnode = bv.walk0;
           if constexpr (kStamps) {
@@ -1052,7 +1041,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
           bool trapped = false;
           pbi = sweep_linear<true>(geo, a.n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(),
                                    pbt, bv.fixpoint ? hint : -1, &trapped);
-          cs.spheres += a.n;
+          cs.fp64 += a.n;
           resolved = true;
           const double am = __builtin_fmax(__builtin_fabs(ox),
                                            __builtin_fmax(__builtin_fabs(oy), __builtin_fabs(oz)));
@@ -1073,16 +1062,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
         __builtin_amdgcn_s_setprio(kWalkPrio);
         if (pending) {
           clk.util(kUWalk);
-#if PSRT_ABLATE == 2
-          {
-            double bt2 = pbt;
-            int bi2 = pbi, n2 = wnode;
-            CullStatsT<false> cs2{0u, 0u};
-            hit_traverse<false, kLds>(bv, nodes, lleaf, sv, hint, ox, oy, oz, dx, dy, dz,
-                                      A, bt2, bi2, cs2, n2, movable ? kWalkTail : 0u, (double)wt0);
-            ablate_sink(bt2), ablate_sink(bi2), ablate_sink(n2);
-          }
-#endif
+          PSRT_ABLATE_AT(WALK);
           hit_traverse<kStamps, kLds>(bv, nodes, lleaf, sv, hint, ox, oy,
                                                          oz, dx, dy, dz, A, pbt, pbi, cs, wnode,
                                                          movable ? kWalkTail : 0u, (double)wt0);
@@ -1118,32 +1098,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
     // without a trial then keeps its resolved hit and scatters in a later
     // iteration (sc_wait): its draws stay in stream order either way.
     const bool want = (resolved && !finish) || sc_wait;
-#if PSRT_ABLATE == 3
-    {
-      const bool can_fill = active && !finish;
-      uint64_t rng2 = rng;
-      uint32_t a0x = q0x, a0y = q0y, a0z = q0z, a1x = q1x, a1y = q1y, a1z = q1z;
-      bool v0 = qv0, v1 = qv1;
-      int f = 0;
-      do {
-        const bool go = can_fill && !v1;
-        uint32_t z, y, x;
-        uint64_t nxt;
-        raw32_x3(rng2, z, y, x, nxt);
-        const bool in = in_unit_sphere_raw_f32(x, y, z);
-        rng2 = go ? nxt : rng2;
-        const bool push = go && in;
-        const bool to0 = push && !v0, to1 = push && v0;
-        a0x = to0 ? x : a0x, a0y = to0 ? y : a0y, a0z = to0 ? z : a0z;
-        a1x = to1 ? x : a1x, a1y = to1 ? y : a1y, a1z = to1 ? z : a1z;
-        v1 = v1 || to1;
-        v0 = v0 || to0;
-        ++f;
-      } while (f < kRngFill || (f < kRngFill + kRngExtra && __ballot(want && !v0) != 0));
-      ablate_sink(rng2), ablate_sink(a0x), ablate_sink(a0y), ablate_sink(a0z);
-      ablate_sink(a1x), ablate_sink(a1y), ablate_sink(a1z), ablate_sink(v0), ablate_sink(v1);
-    }
-#endif
+    PSRT_ABLATE_AT(TRIALS);
     {
       const bool can_fill = active && !finish;
       // branch-free body: every lane computes a trial; only lanes with room
@@ -1173,18 +1128,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
     // ---- scatter: target = (p + n) + random_in_hemisphere(n)  (main.cc:42-43) ----
     const bool have = qv0;
     sc_wait = want && !have;
-#if PSRT_ABLATE == 4
-    if (want && have) {
-      const HitRec h = hit_record_of(sv.geo(hit), sv.inv(hit), t, ox, oy, oz, dx, dy, dz);
-      double rx = pm1_raw(q0x), ry = pm1_raw(q0y), rz = pm1_raw(q0z);
-      if (!((rx * h.nx + ry * h.ny) + rz * h.nz > 0.0)) rx = -rx, ry = -ry, rz = -rz;
-      const double ex = ((h.px + h.nx) + rx) - h.px;
-      const double ey = ((h.py + h.ny) + ry) - h.py;
-      const double ez = ((h.pz + h.nz) + rz) - h.pz;
-      ablate_sink((ex * ex + ey * ey) + ez * ez), ablate_sink(h.px), ablate_sink(h.py);
-      ablate_sink(h.pz);
-    }
-#endif
+    PSRT_ABLATE_AT(SCATTER);
     if (want && have) {
       clk.util(kUScatter);
       const HitRec h = hit_record_of(sv.geo(hit), sv.inv(hit), t, ox, oy, oz, dx, dy, dz);
@@ -1229,13 +1173,14 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
   }
 
   unsigned long long* const ctr = a.ray_counter + kShardStride * (blockIdx.x % kQueues);
-  flush_counters(ctr, rays, cs.spheres, cs.boxes, lane);
+  flush_counters(ctr, rays, cs, lane);
   if (lane == 0 && traced) {
     atomicAdd(ctr, traced);      // the traced rays (the lanes' counters hold the trapped rest)
     atomicAdd(ctr + 3, traced);  // rays_traced
   }
   __syncthreads();  // every wave of the block has left the loop (and flushed to LDS)
-  if (threadIdx.x < 3 && s_flush[threadIdx.x]) atomicAdd(ctr + threadIdx.x, s_flush[threadIdx.x]);
+  if (threadIdx.x < kFlushWords && threadIdx.x != 3 && s_flush[threadIdx.x])
+    atomicAdd(ctr + threadIdx.x, s_flush[threadIdx.x]);
 }
 
 #define PSRT_INSTANTIATE1(B, S, L, C)                                                       \
@@ -1268,7 +1213,7 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
   // sets and queue heads back to zero (ReduceArgs; stream order puts this
   // after every trace block and before the context's next launch)
   if (blockIdx.x == 0 && a.fold_stats) {
-    if (threadIdx.x < 4) {
+    if (threadIdx.x < kStatWords) {
       unsigned long long v = a.first_chunk ? 0ull : a.totals[threadIdx.x];
       for (int h = 0; h < kQueues; ++h) {
         v += a.sets[kShardStride * h + threadIdx.x];
@@ -1338,13 +1283,7 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
         const unsigned p = kPT * i + lane / kLT, j = (lane % kLT) * 2;
         vt[i] = make_double2(0.0, 0.0);
         if (q0 + p < a.pixels && j < T) {
-#if PSRT_REDUCE_NT
-          typedef double nt2 __attribute__((ext_vector_type(2)));
-          const nt2 x = __builtin_nontemporal_load((const nt2*)(a.samp_t + (size_t)(q0 + p) * S + s0 + j));
-          vt[i] = make_double2(x.x, x.y);
-#else
           vt[i] = *(const double2*)(a.samp_t + (size_t)(q0 + p) * S + s0 + j);
-#endif
         }
       }
 #pragma unroll
@@ -1352,13 +1291,7 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
         const unsigned p = kPK * i + lane / kLK, j = (lane % kLK) * 4;
         vk[i] = make_uint2(0u, 0u);
         if (q0 + p < a.pixels && j < T) {
-#if PSRT_REDUCE_NT
-          typedef unsigned nu2 __attribute__((ext_vector_type(2)));
-          const nu2 x = __builtin_nontemporal_load((const nu2*)(a.samp_k + (size_t)(q0 + p) * S + s0 + j));
-          vk[i] = make_uint2(x.x, x.y);
-#else
           vk[i] = *(const uint2*)(a.samp_k + (size_t)(q0 + p) * S + s0 + j);
-#endif
         }
       }
     };
@@ -1580,7 +1513,7 @@ __global__ void psrt_probe_hit(const double4* __restrict__ geo, const double* __
   double t;
   int i;
   if (use_bvh && r[6] == 0.0 && r[7] == __builtin_inf()) {  // the trace kernel's call shape
-    CullStats cs{0u, 0u};
+    CullStats cs{};
     // hint: the sphere the ray starts on (the trace kernel's previous hit)
     const int hint = hints ? hints[k] : -1;
     i = world_hit_bvh(geo, n, bv, hint >= 0 && hint < n ? hint : -1, ox, oy, oz, dx, dy, dz, A, t,

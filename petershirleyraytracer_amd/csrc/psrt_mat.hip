@@ -46,22 +46,18 @@ constexpr double kTmin = 0.001;
 constexpr int kMatHitPrio = 2;
 constexpr int kMatWalkPrio = 3;
 
-// Section ablation (measurement builds only, PSRT_MAT_ABLATE = section id, as
-// psrt_trace's PSRT_ABLATE): 1 hit_quick_m, 2 the batched walk, 3 the
-// random_in_unit_sphere trial loop, 4 the hit record, 5 the refill's per-lane
-// setup run a second time on laundered copies of their inputs, results sunk.
+// Section ablation for the census: measurement builds only
+// (PSRT_MAT_ABLATE = section id, psrt_ablate.h: 1 hit_quick_m, 2 the batched
+// walk, 3 the random_in_unit_sphere trial loop, 4 the hit record, 5 the
+// refill's per-lane setup); in the product build every hook is empty.
 #ifndef PSRT_MAT_ABLATE
 #define PSRT_MAT_ABLATE 0
 #endif
-template <class T>
-__device__ __forceinline__ void mat_sink(T v) {
-  asm volatile("" ::"v"(v));
-}
-template <class T>
-__device__ __forceinline__ T mat_launder(T v) {
-  asm volatile("" : "+v"(v));
-  return v;
-}
+#if PSRT_MAT_ABLATE
+#include "psrt_ablate.h"
+#else
+#define PSRT_MAT_ABLATE_AT(site)
+#endif
 
 __device__ __forceinline__ unsigned div_fast(unsigned n, const FastDiv& f) {
   const unsigned t = __umulhi(f.m, n);
@@ -115,7 +111,8 @@ __device__ __forceinline__ void test_sphere_m(const double4 s, int idx, double o
 // crosses; tmin = 0.001 only removes roots). Returns true when the closest hit
 // is decided (bt, bi); false when the BVH must be walked from (bt, bi).
 template <bool kBVH, bool kCount>
-__device__ __forceinline__ bool hit_quick_m(TestCount<kCount>& nt, const double4* __restrict__ geo,
+__device__ __forceinline__ bool hit_quick_m(TestCount<kCount>& nt, TestCount<kCount>& nr,
+                                            const double4* __restrict__ geo,
                                             int n, const BvhView& bv,
                                             const int* __restrict__ big_idx, const GridC& gc,
                                             uint4 rec, double ox, double oy, double oz, double dx,
@@ -164,13 +161,17 @@ __device__ __forceinline__ bool hit_quick_m(TestCount<kCount>& nt, const double4
     return true;
   }
   // far origin: the segment [0, bt] against the padded root box (FP64)
-  if (!(am <= bv.r_check) && root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt) < 0.0) return true;
+  if (!(am <= bv.r_check)) {
+    nr.add(1u);
+    if (root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt) < 0.0) return true;
+  }
   return false;
 }
 
 // The BVH walk (stackless skip links) continuing from hit_quick_m's (bt, bi).
 template <bool kCount>
 __device__ __forceinline__ void hit_walk_m(TestCount<kCount>& nt, TestCount<kCount>& nb,
+                                           TestCount<kCount>& nr,
                                            const BvhView& bv, const float4* __restrict__ nodes,
                                            const double4* __restrict__ leaf_geo,
                                            const int* __restrict__ leaf_idx, double ox, double oy,
@@ -182,7 +183,10 @@ __device__ __forceinline__ void hit_walk_m(TestCount<kCount>& nt, TestCount<kCou
   // FP32 slab test then sees coordinates of the scene's scale (hit_quick_m
   // has shown the entry exists)
   double t0 = 0.0;
-  if (!(am <= bv.r_check)) t0 = __builtin_fmax(0.0, root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt));
+  if (!(am <= bv.r_check)) {
+    nr.add(1u);
+    t0 = __builtin_fmax(0.0, root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt));
+  }
   const float fox = (float)(ox + t0 * dx), foy = (float)(oy + t0 * dy), foz = (float)(oz + t0 * dz);
   const float ix = safe_inv((float)dx), iy = safe_inv((float)dy), iz = safe_inv((float)dz);
   const float oix = fox * ix, oiy = foy * iy, oiz = foz * iz;
@@ -350,7 +354,9 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
   bool pending = false;
   int pbi = -1;
   double pbt = 0.0;
-  TestCount<kCount> ntests, nboxes;  // RT_FLAG_CULL_STATS: executed sphere / box tests
+  // RT_FLAG_CULL_STATS: executed FP64 sphere tests (every test here is a full
+  // one: no pre-reject), FP32 box tests, FP64 root-box tests
+  TestCount<kCount> ntests, nboxes, nroots;
 
   for (;;) {
     // ---- refill idle lanes from the wave's window (ballot + mbcnt) ----
@@ -381,17 +387,7 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
         if (unit < total) {
           su = (unsigned)unit;
           setup(su, rng, ox, oy, oz, dx, dy, dz, A, pq);
-#if PSRT_MAT_ABLATE == 5
-          {
-            uint64_t r2;
-            double o2x, o2y, o2z, d2x, d2y, d2z, A2;
-            unsigned q2;
-            setup(mat_launder(su), r2, o2x, o2y, o2z, d2x, d2y, d2z, A2, q2);
-            mat_sink(q2);
-            mat_sink(r2), mat_sink(o2x), mat_sink(o2y), mat_sink(o2z), mat_sink(d2x),
-                mat_sink(d2y), mat_sink(d2z), mat_sink(A2);
-          }
-#endif
+          PSRT_MAT_ABLATE_AT(SETUP);
           k = 0;
           np = 0;
           active = true;
@@ -426,19 +422,9 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
         __builtin_amdgcn_s_setprio(kMatHitPrio);
         uint4 rec = make_uint4(kCamOverflow, 0u, 0u, 0u);
         if (k == 0 && a.plist) rec = a.plist[pq];  // camera ray: its pixel's list
-        decided = hit_quick_m<kBVH>(ntests, lgeo, a.n, bv, big_idx, gc, rec, ox, oy, oz, dx, dy,
-                                    dz, A, pbt, pbi);
-#if PSRT_MAT_ABLATE == 1
-        {
-          double bt2;
-          int bi2;
-          const bool d2 = hit_quick_m<kBVH>(ntests, lgeo, a.n, bv, big_idx, gc, rec, mat_launder(ox),
-                                            mat_launder(oy), mat_launder(oz), mat_launder(dx),
-                                            mat_launder(dy), mat_launder(dz), mat_launder(A), bt2,
-                                            bi2);
-          mat_sink(bt2), mat_sink(bi2), mat_sink(d2);
-        }
-#endif
+        decided = hit_quick_m<kBVH>(ntests, nroots, lgeo, a.n, bv, big_idx, gc, rec, ox, oy, oz,
+                                    dx, dy, dz, A, pbt, pbi);
+        PSRT_MAT_ABLATE_AT(HIT);
         __builtin_amdgcn_s_setprio(0);
         pending = !decided;
       }
@@ -449,18 +435,10 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
                         __ballot(active && !pending && !fin) == 0)) {
         __builtin_amdgcn_s_setprio(kMatWalkPrio);
         if (pending) {
-#if PSRT_MAT_ABLATE == 2
-          double bt2 = mat_launder(pbt);
-          int bi2 = mat_launder(pbi);
-#endif
-          hit_walk_m(ntests, nboxes, bv, nodes, leaf_geo, leaf_idx, ox, oy, oz, dx, dy, dz, A,
-                     pbt, pbi);
-#if PSRT_MAT_ABLATE == 2
-          hit_walk_m(ntests, nboxes, bv, nodes, leaf_geo, leaf_idx, mat_launder(ox), mat_launder(oy),
-                     mat_launder(oz), mat_launder(dx), mat_launder(dy), mat_launder(dz),
-                     mat_launder(A), bt2, bi2);
-          mat_sink(bt2), mat_sink(bi2);
-#endif
+          PSRT_MAT_ABLATE_AT(WALK_SAVE);
+          hit_walk_m(ntests, nboxes, nroots, bv, nodes, leaf_geo, leaf_idx, ox, oy, oz, dx, dy, dz,
+                     A, pbt, pbi);
+          PSRT_MAT_ABLATE_AT(WALK_RUN);
           pending = false;
           decided = true;
         }
@@ -492,16 +470,7 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
     if (resolved) {
       const int bi = pbi;
       const HitRec h = hit_record_of(lgeo[bi], linv[bi], pbt, ox, oy, oz, dx, dy, dz);
-#if PSRT_MAT_ABLATE == 4
-      {
-        const int bi2 = mat_launder(bi);
-        const HitRec h2 = hit_record_of(lgeo[bi2], linv[bi2], mat_launder(pbt), mat_launder(ox),
-                                        mat_launder(oy), mat_launder(oz), mat_launder(dx),
-                                        mat_launder(dy), mat_launder(dz));
-        mat_sink(h2.px), mat_sink(h2.py), mat_sink(h2.pz), mat_sink(h2.nx), mat_sink(h2.ny),
-            mat_sink(h2.nz), mat_sink(h2.front);
-      }
-#endif
+      PSRT_MAT_ABLATE_AT(RECORD);
       const int kind = mat_kind(bi);
       double ndx = 0.0, ndy = 0.0, ndz = 0.0;
       bool ok = true;
@@ -540,25 +509,11 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
         // pre-decision (psrt_device.h in_unit_sphere_raw_f32) was 1.5% slower
         // in this divergent loop (its ballot runs per trial; r04,
         // profiles/r04_mat/ab.txt).
-#if PSRT_MAT_ABLATE == 3
-        {
-          uint64_t r2 = mat_launder(rng);
-          uint32_t z2, y2, x2;
-          for (;;) {
-            raw32_x3(r2, z2, y2, x2, r2);
-            if (in_unit_sphere_raw(x2, y2, z2)) break;
-          }
-          mat_sink(z2), mat_sink(y2), mat_sink(x2), mat_sink(r2);
-        }
-#endif
+        PSRT_MAT_ABLATE_AT(TRIALS);
         uint32_t rz, ry, rx;
         for (;;) {
           raw32_x3(rng, rz, ry, rx, rng);
-#ifdef PSRT_MAT_TRIAL_F32  // A/B build
-          if (in_unit_sphere_raw_f32(rx, ry, rz)) break;
-#else
           if (in_unit_sphere_raw(rx, ry, rz)) break;
-#endif
         }
         // random(-1, 1) of each draw, exact from the raw value (psrt_device.h)
         const double x = pm1_raw(rx), y = pm1_raw(ry), z = pm1_raw(rz);
@@ -610,11 +565,13 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
     atomicAdd(ctr + 3, rays);
   }
   if constexpr (kCount) {
-    unsigned long long t = ntests.v, b = nboxes.v;
-    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off), b += __shfl_xor(b, off);
+    unsigned long long t = ntests.v, b = nboxes.v, r = nroots.v;
+    for (int off = 32; off > 0; off >>= 1)
+      t += __shfl_xor(t, off), b += __shfl_xor(b, off), r += __shfl_xor(r, off);
     if (lane == 0) {
       atomicAdd(ctr + 1, t);
       atomicAdd(ctr + 2, b);
+      atomicAdd(ctr + 5, r);
     }
   }
 }
@@ -635,7 +592,7 @@ PSRT_MAT_INSTANTIATE(true, true)
 // folds the trace launch's counter sets as psrt_reduce does.
 __global__ __launch_bounds__(kReduceBlock) void psrt_reduce_rgb(ReduceArgs a) {
   if (blockIdx.x == 0 && a.fold_stats) {
-    if (threadIdx.x < 4) {
+    if (threadIdx.x < kStatWords) {
       unsigned long long v = a.first_chunk ? 0ull : a.totals[threadIdx.x];
       for (int h = 0; h < kQueues; ++h) {
         v += a.sets[kShardStride * h + threadIdx.x];

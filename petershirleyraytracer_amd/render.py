@@ -19,6 +19,7 @@ cameras are ``(4, 3)`` float64 arrays (origin, lower_left, horizontal, vertical)
 from __future__ import annotations
 
 import ctypes as C
+from contextlib import contextmanager
 from dataclasses import dataclass
 from typing import Optional
 
@@ -213,7 +214,8 @@ def save_scene(path: str, spheres, camera=None, **render_args) -> None:
 def stats_dict(s: RtStats) -> dict:
     return dict(samples=s.samples, rays=s.rays, sphere_tests=s.sphere_tests,
                 tests_executed=s.tests_executed, box_tests=s.box_tests,
-                kernel_ms=s.kernel_ms, total_ms=s.total_ms, rays_traced=s.rays_traced)
+                kernel_ms=s.kernel_ms, total_ms=s.total_ms, rays_traced=s.rays_traced,
+                prerejects=s.prerejects, root_box_tests=s.root_box_tests)
 
 
 def render(spheres, camera, width: int, height: int, spp: int, max_depth: int = 50,
@@ -269,6 +271,36 @@ def render_materials(spheres, materials, camera: LensCamera, width: int, height:
                                 rgb.ctypes.data_as(C.POINTER(C.c_ubyte)) if rgb is not None
                                 else None, C.byref(st)), "rt_render_materials")
     return acc, rgb, stats_dict(st)
+
+
+def set_tuning(name: str, value: float, ctx: Optional["Context"] = None) -> None:
+    """rt_context_set_tuning: a measurement / test knob (include/rt.h) of one
+    context, or (ctx=None) the process defaults that new contexts and the
+    one-shot entries take. Every knob keeps the output bit-identical."""
+    L = _lib.load()
+    check(L.rt_context_set_tuning(ctx.handle if ctx is not None else None, name.encode(),
+                                  float(value)), "rt_context_set_tuning")
+
+
+def get_tuning(name: str, ctx: Optional["Context"] = None) -> float:
+    v = C.c_double()
+    check(_lib.load().rt_context_get_tuning(ctx.handle if ctx is not None else None,
+                                            name.encode(), C.byref(v)), "rt_context_get_tuning")
+    return v.value
+
+
+@contextmanager
+def tuning(**knobs):
+    """Set process-default knobs for the duration of a block (tests, A/B
+    scripts), then restore the previous values."""
+    old = {k: get_tuning(k) for k in knobs}
+    try:
+        for k, v in knobs.items():
+            set_tuning(k, v)
+        yield
+    finally:
+        for k, v in old.items():
+            set_tuning(k, v)
 
 
 def quantize(accum: np.ndarray, spp: int) -> np.ndarray:
@@ -336,6 +368,13 @@ class Context:
         chunk `chunk`'s trace launch, before its reduce (rt_debug_fail_after_trace)."""
         check(self._L.rt_debug_fail_after_trace(self.handle, chunk), "rt_debug_fail_after_trace")
 
+    def set_tuning(self, name: str, value: float) -> None:
+        """rt_context_set_tuning on this context (measurement / test knobs)."""
+        set_tuning(name, value, self)
+
+    def get_tuning(self, name: str) -> float:
+        return get_tuning(name, self)
+
     def stream(self) -> int:
         """The context's own hipStream_t (as an int), used for stream=0."""
         return self._L.rt_context_stream(self.handle) or 0
@@ -360,6 +399,70 @@ class Context:
             self.close()
         except Exception:
             pass
+
+
+class DeviceGroup:
+    """rt_group (include/rt.h): one frame over several devices natively, one
+    context and host thread per member, interleaved rows gathered into
+    reference pixel order in host memory. Members may repeat a device."""
+
+    def __init__(self, devices):
+        self._L = _lib.load()
+        devs = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        check(self._L.rt_group_create(devs, len(devices), C.byref(h)), "rt_group_create")
+        self.handle = h
+        self.devices = list(devices)
+
+    def set_scene(self, spheres, camera) -> None:
+        sp, n = _spheres(spheres)
+        cam = _camera(camera)
+        check(self._L.rt_group_set_scene(self.handle, sp, n, C.byref(cam)), "rt_group_set_scene")
+
+    def render(self, width: int, height: int, spp: int, max_depth: int = 50, seed: int = 0,
+               row_offset: int = 0, row_stride: int = 1, flags: int = 0, want_rgb: bool = True):
+        """Returns (accum[rows, W, 3], rgb8 or None, stats) of the shard."""
+        p = params(width, height, spp, max_depth, seed, row_offset, row_stride, flags)
+        rows = max(0, self._L.rt_rows_owned(height, row_offset, row_stride))
+        acc = np.zeros((rows, width, 3), dtype=np.float64)
+        rgb = np.zeros((rows, width, 3), dtype=np.uint8) if want_rgb else None
+        st = RtStats()
+        check(self._L.rt_group_render(self.handle, C.byref(p),
+                                      acc.ctypes.data_as(C.POINTER(C.c_double)),
+                                      rgb.ctypes.data_as(C.POINTER(C.c_ubyte))
+                                      if rgb is not None else None, C.byref(st)),
+              "rt_group_render")
+        return acc, rgb, stats_dict(st)
+
+    def close(self) -> None:
+        if self.handle:
+            self._L.rt_group_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def render_devices(spheres, camera, width: int, height: int, spp: int, devices,
+                   max_depth: int = 50, seed: int = 0, row_offset: int = 0, row_stride: int = 1):
+    """rt_render_devices: one-shot render of the shard over `devices`."""
+    L = _lib.load()
+    sp, n = _spheres(spheres)
+    cam = _camera(camera)
+    p = params(width, height, spp, max_depth, seed, row_offset, row_stride)
+    rows = max(0, L.rt_rows_owned(height, row_offset, row_stride))
+    acc = np.zeros((rows, width, 3), dtype=np.float64)
+    rgb = np.zeros((rows, width, 3), dtype=np.uint8)
+    st = RtStats()
+    devs = (C.c_int * len(devices))(*devices)
+    check(L.rt_render_devices(sp, n, C.byref(cam), C.byref(p), devs, len(devices),
+                              acc.ctypes.data_as(C.POINTER(C.c_double)),
+                              rgb.ctypes.data_as(C.POINTER(C.c_ubyte)), C.byref(st)),
+          "rt_render_devices")
+    return acc, rgb, stats_dict(st)
 
 
 def ppm_p3(rgb8: np.ndarray) -> bytes:

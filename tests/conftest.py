@@ -53,6 +53,24 @@ def oracle_mod():
     return oracle
 
 
+@pytest.fixture
+def knobs():
+    """Set process-default tuning knobs (rt_context_set_tuning(NULL, ...),
+    include/rt.h) for one test: contexts created afterwards and the one-shot
+    entries take them; the previous values come back at teardown."""
+    import petershirleyraytracer_amd as P
+    saved = {}
+
+    def set_(name, value):
+        if name not in saved:
+            saved[name] = P.get_tuning(name)
+        P.set_tuning(name, value)
+
+    yield set_
+    for k, v in saved.items():
+        P.set_tuning(k, v)
+
+
 def have_gpu() -> bool:
     try:
         import petershirleyraytracer_amd as P

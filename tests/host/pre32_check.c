@@ -4,10 +4,18 @@
  * radius 1e-3 .. 1e3 (the r = 1000 ground included), directions towards the
  * sphere, bt spread around D / |d|. Every rejected case must have no accepted
  * root; the device's v_sqrt_f32 (1 ulp) is modelled by rounding sqrt down 2 ulp.
- * Prints "ok <cases> <rejected>" or the first violations. */
+ * The whole configuration is also scaled down by 2^-20 .. 2^-90 (ADVICE r04:
+ * below ~2^-57 an absolute floor of 2^-100 in R let T*T lose its relative
+ * accuracy; the floor is 2^-60, so T*T >= 2^-120 stays a normal float).
+ * Prints "ok <cases> <rejected>" or the first violations.
+ * -DR_FLOOR=0x1p-100 builds the old floor (it fails at the tiny scales). */
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+
+#ifndef R_FLOOR
+#define R_FLOOR 0x1p-60 /* psrt_capi.hip pre32_sphere */
+#endif
 
 static uint64_t st = 0x9E3779B97F4A7C15ull;
 static double u01(void) {
@@ -19,7 +27,7 @@ static double u01(void) {
 static float pre32_R(double cx, double cy, double cz, double r) {
   const double ar = fabs(r), cm = fmax(fabs(cx), fmax(fabs(cy), fabs(cz)));
   if (!(cm + ar <= 0x1p40)) return INFINITY;
-  const double Rd = ar * (1.0 + 0x1p-18) + 0x1p-18 * cm + 0x1p-100;
+  const double Rd = ar * (1.0 + 0x1p-18) + 0x1p-18 * cm + R_FLOOR;
   float R = (float)Rd;
   if ((double)R < Rd) R = nextafterf(R, INFINITY);
   return R;
@@ -60,7 +68,11 @@ static int ref_hit(double ox, double oy, double oz, double dx, double dy, double
 
 int main(void) {
   long cases = 0, rej = 0, bad = 0;
-  for (int it = 0; it < 4000000; ++it) {
+  /* 4 M cases at scale 1, then 600 k at each smaller scale */
+  static const double scales[] = {0x1p-20, 0x1p-40, 0x1p-57, 0x1p-64, 0x1p-70, 0x1p-80, 0x1p-90};
+  const int n_scaled = 600000, n_plain = 4000000;
+  for (int it = 0; it < n_plain + 7 * n_scaled; ++it) {
+    const double S = it < n_plain ? 1.0 : scales[(it - n_plain) / n_scaled];
     double cx, cy, cz, r;
     const int kind = it % 4;
     if (kind == 0) {
@@ -75,8 +87,9 @@ int main(void) {
     const double nl = sqrt(nx * nx + ny * ny + nz * nz);
     nx /= nl, ny /= nl, nz /= nl;
     const double D = pow(10.0, -13.0 + 15.0 * u01());
-    const double ar = fabs(r);
-    const double ox = cx + nx * (ar + D), oy = cy + ny * (ar + D), oz = cz + nz * (ar + D);
+    cx *= S, cy *= S, cz *= S, r *= S;
+    const double ar = fabs(r), Ds = D * S;
+    const double ox = cx + nx * (ar + Ds), oy = cy + ny * (ar + Ds), oz = cz + nz * (ar + Ds);
     /* direction: towards the sphere (the centre, jittered), or random */
     double dx, dy, dz;
     if (it % 3) {
@@ -89,7 +102,7 @@ int main(void) {
     const double A = (dx * dx + dy * dy) + dz * dz;
     const double am = fmax(fabs(ox), fmax(fabs(oy), fabs(oz)));
     /* bt around D / |d|: 0, tiny, and D/|d| * (1 +- 2^-k) */
-    const double base = D / sqrt(A);
+    const double base = Ds / sqrt(A);
     double bt;
     switch (it % 5) {
       case 0: bt = 0.0; break;

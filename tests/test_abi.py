@@ -36,7 +36,7 @@ def test_exports_every_declared_symbol():
 
 def test_abi_version_and_info():
     L = _lib.load()
-    assert L.rt_abi_version() == 4
+    assert L.rt_abi_version() == 5
     assert b"gfx950" in L.rt_build_info()
 
 
@@ -131,3 +131,40 @@ def test_product_does_not_import_oracle():
                 txt = open(os.path.join(dp, f)).read()
                 assert "import oracle" not in txt and "liboracle" not in txt, f
                 assert "oracle/" not in txt, f
+
+
+def test_tuning_knobs_without_device():
+    """rt_context_set_tuning / get_tuning on the process defaults (ctx NULL)
+    need no device: round trip, unknown names and non-finite values fail."""
+    old = P.get_tuning("queue_k")
+    assert old == 2.0 and P.get_tuning("sample_buf_mb") == 49152.0
+    with P.tuning(queue_k=3.5, no_camlist=1):
+        assert P.get_tuning("queue_k") == 3.5 and P.get_tuning("no_camlist") == 1.0
+    assert P.get_tuning("queue_k") == old and P.get_tuning("no_camlist") == 0.0
+    with pytest.raises(_lib.RtError, match="unknown knob"):
+        P.set_tuning("no_such_knob", 1)
+    with pytest.raises(_lib.RtError, match="finite"):
+        P.set_tuning("queue_k", float("nan"))
+
+
+def test_render_path_reads_no_environment():
+    """The library's knobs go through rt_context_set_tuning: no getenv in the
+    product sources except RT_DEVICE (the one-shot entries' device, read once,
+    include/rt.h)."""
+    csrc = os.path.join(ROOT, "petershirleyraytracer_amd", "csrc")
+    for dp, _, fs in os.walk(csrc):
+        for f in fs:
+            if not f.endswith((".hip", ".cpp", ".h", ".cc")):
+                continue
+            for m in re.finditer(r"getenv\(([^)]*)\)", open(os.path.join(dp, f)).read()):
+                assert m.group(1) == '"RT_DEVICE"', (f, m.group(0))
+
+
+def test_census_hooks_are_out_of_the_product_kernels():
+    """The census's section duplicates live in psrt_ablate.h, included only by
+    measurement builds (PSRT_ABLATE / PSRT_MAT_ABLATE non-zero)."""
+    csrc = os.path.join(ROOT, "petershirleyraytracer_amd", "csrc")
+    for f in ("psrt_kernels.hip", "psrt_mat.hip"):
+        txt = open(os.path.join(csrc, f)).read()
+        assert re.search(r"#if PSRT_(MAT_)?ABLATE ==", txt) is None, f
+        assert "ablate_sink" not in txt, f

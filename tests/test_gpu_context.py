@@ -5,7 +5,7 @@
   buffer reallocation never touches buffers an in-flight render still reads.
 - rt_render is safe to call from several host threads (per-device lock).
 - The kernel's 32-bit per-lane counters flush to the 64-bit totals before
-  they can wrap (PSRT_FLUSH_AT forces the flush path on every refill block).
+  they can wrap (the flush_at tuning knob forces the flush path on every refill block).
 - A shard that owns no rows (more ranks than rows) renders nothing.
 
 Expected values come from the oracle restatement (pinned to the reference's
@@ -92,7 +92,7 @@ def test_rt_render_from_threads(oracle_mod):
 
 
 @pytest.mark.parametrize("flush_at", ["1", "7"])
-def test_counter_flush_keeps_totals(oracle_mod, monkeypatch, flush_at):
+def test_counter_flush_keeps_totals(oracle_mod, knobs, flush_at):
     """rays / tests stay exact when the per-lane counters flush mid-launch,
     also at max_depth 100000 (trapped paths add max_depth - k at once)."""
     two = oracle_mod.scene_two_spheres()
@@ -102,9 +102,9 @@ def test_counter_flush_keeps_totals(oracle_mod, monkeypatch, flush_at):
     base = {}
     for key, (s, c, w, h, n, d) in {"two": (two, cam, 40, 20, 3, 100000),
                                      "fin": (fin, cam_f, 48, 32, 4, 50)}.items():
-        monkeypatch.delenv("PSRT_FLUSH_AT", raising=False)
+        knobs("flush_at", 0)
         acc0, _, st0 = P.render(s, c, w, h, n, d, cull_stats=True)
-        monkeypatch.setenv("PSRT_FLUSH_AT", flush_at)
+        knobs("flush_at", int(flush_at))
         acc1, _, st1 = P.render(s, c, w, h, n, d, cull_stats=True)
         assert np.array_equal(bits(acc0), bits(acc1)), key
         for f in ("rays", "tests_executed", "box_tests", "rays_traced"):
@@ -165,7 +165,7 @@ def test_render_into_pinned_host_memory():
 
 
 @pytest.mark.parametrize("buf_mb", [None, "1"])
-def test_multi_frame_launch_equals_single_frames(monkeypatch, buf_mb):
+def test_multi_frame_launch_equals_single_frames(knobs, buf_mb):
     """rt_render_device_frames: frame f of a batch is bit for bit the frame of
     seed + f rendered alone (per-frame seeds, frame-major units, one stats
     fold), for a shard of the final scene, in one sample chunk and (1 MB
@@ -176,7 +176,7 @@ def test_multi_frame_launch_equals_single_frames(monkeypatch, buf_mb):
     cam = P.camera_look_at(aspect=w / h)
     rows = P.rows_owned(h, 1, 3)
     if buf_mb:
-        monkeypatch.setenv("PSRT_SAMPLE_BUF_MB", buf_mb)
+        knobs("sample_buf_mb", int(buf_mb))
     ctx = P.Context(0)
     ctx.set_scene(sph, cam)
     acc = torch.zeros((nf, rows, w, 3), dtype=torch.float64, device="cuda:0")
@@ -206,7 +206,7 @@ def test_multi_frame_launch_equals_single_frames(monkeypatch, buf_mb):
 
 
 @pytest.mark.parametrize("fail_at", ["0", "1"])
-def test_render_after_a_failure_mid_render(oracle_mod, monkeypatch, fail_at):
+def test_render_after_a_failure_mid_render(oracle_mod, knobs, fail_at):
     """A render that fails after a trace launch and before its reduce (the
     rt_debug_fail_after_trace hook stands in for a HIP error there) leaves the
     queue heads and counter sets non-zero: the context is marked dirty, and
@@ -216,7 +216,7 @@ def test_render_after_a_failure_mid_render(oracle_mod, monkeypatch, fail_at):
     sph = oracle_mod.scene_random_spheres(1)
     w, h, spp = 48, 32, 150
     cam = oracle_mod.camera_look_at(aspect=w / h)
-    monkeypatch.setenv("PSRT_SAMPLE_BUF_MB", "1")  # 68 samples of 1536 pixels: chunks of 52, 52, 46
+    knobs("sample_buf_mb", 1)  # 68 samples of 1536 pixels: chunks of 52, 52, 46
     ctx = P.Context(0)
     ctx.set_scene(sph, cam)
     acc = torch.zeros((h, w, 3), dtype=torch.float64, device="cuda:0")
@@ -232,4 +232,35 @@ def test_render_after_a_failure_mid_render(oracle_mod, monkeypatch, fail_at):
     want, _, rays = oracle_mod.render(sph, cam, w, h, spp, 50, 3, threads=8)
     assert np.array_equal(bits(acc.cpu().numpy()), bits(want))
     assert st["rays"] == rays and st["samples"] == w * h * spp
+    ctx.close()
+
+
+def test_multi_frame_overlapping_buffers_keep_frame_order():
+    """Frames whose accumulator / byte blocks overlap (a stride below one
+    frame) are not reduced concurrently: the per-frame reduces
+    run in frame order, so each later frame overwrites the overlap as a
+    sequence of one-frame renders would."""
+    import torch
+    sph = P.scene_random_spheres(1)
+    w, h, spp, nf = 32, 16, 4, 3
+    cam = P.camera_look_at(aspect=w / h)
+    P3 = w * h * 3
+    half = P3 // 2  # frame f starts half a frame after frame f - 1
+    acc = torch.zeros(half * (nf - 1) + P3, dtype=torch.float64, device="cuda:0")
+    rgb = torch.zeros(half * (nf - 1) + P3, dtype=torch.uint8, device="cuda:0")
+    ctx = P.Context(0)
+    ctx.set_scene(sph, cam)
+    ctx.render_device_frames(P.params(w, h, spp, 50, 11), nf,
+                             [acc.data_ptr() + 8 * half * f for f in range(nf)],
+                             [rgb.data_ptr() + half * f for f in range(nf)])
+    ctx.sync_stats()
+    torch.cuda.synchronize()
+    want_acc = np.zeros(acc.shape, dtype=np.float64)
+    want_rgb = np.zeros(rgb.shape, dtype=np.uint8)
+    for f in range(nf):
+        a, r, _ = P.render(sph, cam, w, h, spp, 50, 11 + f)
+        want_acc[half * f:half * f + P3] = a.reshape(-1)
+        want_rgb[half * f:half * f + P3] = r.reshape(-1)
+    assert np.array_equal(bits(acc.cpu().numpy()), bits(want_acc))
+    assert np.array_equal(rgb.cpu().numpy(), want_rgb)
     ctx.close()

@@ -244,6 +244,9 @@ def test_trapped_termination_is_bit_identical(oracle_mod, final_scene):
     assert sa["rays"] == sb["rays"]
     assert sa["tests_executed"] < sb["tests_executed"] / 2, (sa, sb)
     assert sb["rays_traced"] == sb["rays"] and sa["rays_traced"] < sa["rays"] / 3, (sa, sb)
+    # the counting variant's tallies by kind (bench.py's roofline): FP32
+    # pre-rejects, FP32 slab tests and FP64 root-box tests all occur on C3's scene
+    assert sa["prerejects"] > 0 and sa["box_tests"] > 0 and sa["root_box_tests"] > 0, sa
     want, _, rays = oracle_mod.render(final_scene, cam, 160, 90, 8, threads=8)
     assert np.array_equal(bits(a), bits(want)) and sa["rays"] == rays
 
@@ -276,7 +279,7 @@ def test_trapped_termination_contact_scenes(oracle_mod, seed):
     assert np.array_equal(bits(a), bits(want)) and sa["rays"] == rays
 
 
-def test_camera_lists_are_bit_identical(oracle_mod, final_scene, monkeypatch):
+def test_camera_lists_are_bit_identical(oracle_mod, final_scene, knobs):
     """camera rays tested against per-pixel candidate lists give
     the same frame as the BVH walk, for the benchmark camera and for cameras
     close to / inside spheres, wide and narrow fields, and a 1:3 shard."""
@@ -287,16 +290,16 @@ def test_camera_lists_are_bit_identical(oracle_mod, final_scene, monkeypatch):
     for cam in cams:
         for off, stride in ((0, 1), (1, 3)):
             a, _, sa = P.render(final_scene, cam, 96, 64, 3, row_offset=off, row_stride=stride)
-            monkeypatch.setenv("PSRT_NO_CAMLIST", "1")
+            knobs("no_camlist", 1)
             b, _, sb = P.render(final_scene, cam, 96, 64, 3, row_offset=off, row_stride=stride)
-            monkeypatch.delenv("PSRT_NO_CAMLIST")
+            knobs("no_camlist", 0)
             assert np.array_equal(bits(a), bits(b)) and sa["rays"] == sb["rays"]
             want, _, rays = oracle_mod.render(final_scene, cam, 96, 64, 3, row_offset=off,
                                               row_stride=stride, threads=8)
             assert np.array_equal(bits(a), bits(want)) and sa["rays"] == rays
 
 
-def test_neighbour_lists_are_bit_identical(oracle_mod, final_scene, monkeypatch):
+def test_neighbour_lists_are_bit_identical(oracle_mod, final_scene, knobs):
     """rays that re-hit their start sphere test only its
     neighbours; the frames equal the grid/BVH path's and the oracle's, on the
     final scene and on contact scenes (touching, duplicate, nested spheres)."""
@@ -307,9 +310,26 @@ def test_neighbour_lists_are_bit_identical(oracle_mod, final_scene, monkeypatch)
                                         aspect=96 / 64)))
     for sph, cam in scenes:
         a, _, sa = P.render(sph, cam, 96, 64, 4)
-        monkeypatch.setenv("PSRT_NO_NEIGHBORS", "1")
+        knobs("no_neighbors", 1)
         b, _, sb = P.render(sph, cam, 96, 64, 4)
-        monkeypatch.delenv("PSRT_NO_NEIGHBORS")
+        knobs("no_neighbors", 0)
         assert np.array_equal(bits(a), bits(b)) and sa["rays"] == sb["rays"]
         want, _, rays = oracle_mod.render(sph, cam, 96, 64, 4, threads=8)
         assert np.array_equal(bits(a), bits(want)) and sa["rays"] == rays
+
+
+def test_far_camera_rebase_bit_exact(oracle_mod, final_scene):
+    """A camera ~1.4e10 units out (2^30 x the book's lookfrom, a field of
+    view 2^-30 of 20 degrees): every camera ray is a far origin whose
+    root-box entry, kept as a float, would move the re-based origin far
+    outside the range the FP32 slab test's error bound covers.
+    Such entries are recomputed in FP64 by the walk; the frame equals the
+    oracle's, and the counting variant sees the FP64 root-box tests."""
+    lf = tuple(np.array([13.0, 2.0, 3.0]) * 2.0 ** 30)
+    cam = P.camera_look_at(lf, (0.0, 0.5, 0.0), vfov=20.0 * 2.0 ** -30, aspect=48 / 32)
+    assert np.abs(cam[0]).max() > 1e10
+    a, _, sa = P.render(final_scene, cam, 48, 32, 3, seed=5, cull_stats=True)
+    want, _, rays = oracle_mod.render(final_scene, cam, 48, 32, 3, seed=5, threads=8)
+    assert np.array_equal(bits(a), bits(want)) and sa["rays"] == rays
+    assert sa["root_box_tests"] >= 48 * 32 * 3  # every camera ray, at least once
+    assert sa["tests_executed"] > 0 and sa["prerejects"] > 0

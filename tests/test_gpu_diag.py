@@ -1,4 +1,4 @@
-"""The diagnostic kernel variant (PSRT_STAMPS=1: psrt_trace<kStamps = true>,
+"""The diagnostic kernel variant (tuning knob stamps = 1: psrt_trace<kStamps = true>,
 DESIGN.md §4 section clocks, lane-utilisation probes and the wave timeline)
 renders the same bits and rays as the product kernel and prints its
 measurement lines. It is the only non-default variant the library builds
@@ -14,12 +14,12 @@ from conftest import bits
 pytestmark = pytest.mark.gpu
 
 
-def test_stamps_variant_same_bits_and_reports(final_scene, monkeypatch, capfd):
+def test_stamps_variant_same_bits_and_reports(final_scene, knobs, capfd):
     cam = P.camera_look_at(aspect=96 / 64)
     a, ra, sa = P.render(final_scene, cam, 96, 64, 4)
-    monkeypatch.setenv("PSRT_STAMPS", "1")
+    knobs("stamps", 1)
     b, rb, sb = P.render(final_scene, cam, 96, 64, 4)
-    monkeypatch.delenv("PSRT_STAMPS")
+    knobs("stamps", 0)
     assert np.array_equal(bits(a), bits(b)) and np.array_equal(ra, rb)
     assert (sa["rays"], sa["rays_traced"]) == (sb["rays"], sb["rays_traced"])
     err = capfd.readouterr().err

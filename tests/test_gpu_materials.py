@@ -30,11 +30,11 @@ def book(oracle_mod):
 
 
 @pytest.mark.parametrize("cull,lds", [(True, None), (True, "0"), (False, None)])
-def test_book_scene_bit_exact(oracle_mod, book, cull, lds, monkeypatch):
+def test_book_scene_bit_exact(oracle_mod, book, cull, lds, knobs):
     """The culled kernel with the scene in LDS (default) and in global memory
-    (PSRT_MAT_LDS=0), and the linear scan."""
+    (tuning knob mat_lds = 0), and the linear scan."""
     if lds is not None:
-        monkeypatch.setenv("PSRT_MAT_LDS", lds)
+        knobs("mat_lds", int(lds))
     sp, mt, lens = book
     W, H, spp, seed = 72, 48, 4, 9
     acc, rgb, st = P.render_materials(sp, mt, _lens(lens), W, H, spp, 50, seed, cull=cull)
@@ -68,14 +68,14 @@ def test_shards_and_depth_edges(oracle_mod, book):
         P.render_materials(sp, mt, _lens(lens), W, H, spp, 4097, 4)
 
 
-def test_chunked_multi_frame_context(oracle_mod, book, monkeypatch):
+def test_chunked_multi_frame_context(oracle_mod, book, knobs):
     """Sample chunks (a small buffer cap) and multi-frame launches through the
     context: frame f equals the one-shot render of seed + f."""
     import torch
     sp, mt, lens = book
     W, H, spp, seed, nf = 32, 20, 48, 21, 3
     # 1 MiB holds 22 samples of 3 frames x 640 pixels x 24 B: 3 chunks of 16
-    monkeypatch.setenv("PSRT_SAMPLE_BUF_MB", "1")
+    knobs("sample_buf_mb", 1)
     ctx = P.Context(0)
     try:
         ctx.set_scene(sp, lens["base"])
@@ -133,16 +133,16 @@ def test_long_paths_between_mirrors(oracle_mod):
 
 
 @pytest.mark.parametrize("aperture", [0.1, 2.0, 0.0])
-def test_apertures_bit_exact(oracle_mod, book, monkeypatch, aperture):
+def test_apertures_bit_exact(oracle_mod, book, knobs, aperture):
     """The book's aperture, a wide one and a pinhole, at 240 x 160 x 6.
     Camera rays through the lens test only their pixel's candidate list
     (psrt_mat_camera_lists): the frame equals the one without
-    lists (PSRT_NO_CAMLIST) bit for bit, and the oracle's."""
+    lists (tuning knob no_camlist) bit for bit, and the oracle's."""
     sp, mt, _ = book
     W, H, spp = 240, 160, 6
     lens = oracle_mod.camera_look_at_lens(aspect=W / H, aperture=aperture)
     acc, rgb, st = P.render_materials(sp, mt, _lens(lens), W, H, spp, 50, 13)
-    monkeypatch.setenv("PSRT_NO_CAMLIST", "1")
+    knobs("no_camlist", 1)
     acc2, _, st2 = P.render_materials(sp, mt, _lens(lens), W, H, spp, 50, 13)
     assert np.array_equal(bits(acc), bits(acc2)) and st["rays"] == st2["rays"]
     ref, rays = oracle_mod.render_mat(sp, mt, lens, W, H, spp, 50, 13, threads=8)
@@ -184,5 +184,31 @@ def test_counting_variant_same_bits(oracle_mod, book):
         assert np.array_equal(bits(out[0][0]), bits(out[1][0]))
         assert out[0][1]["tests_executed"] == 0 and out[1][1]["tests_executed"] > out[1][1]["rays"]
         assert out[1][1]["box_tests"] > 0 and out[0][1]["rays"] == out[1][1]["rays"]
+    finally:
+        ctx.close()
+
+
+def test_failure_hook_on_the_material_path(oracle_mod, book):
+    """rt_debug_fail_after_trace fails a RT_FLAG_MATERIALS render after its
+    trace launch, as it does the reference integrator's (the hook
+    was consumed silently); the next render is whole and bit-exact."""
+    import torch
+    sp, mt, lens = book
+    W, H, spp = 40, 24, 3
+    ctx = P.Context(0)
+    try:
+        ctx.set_scene(sp, lens["base"])
+        ctx.set_materials(mt, _lens(lens))
+        acc = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
+        ctx.debug_fail_after_trace(0)
+        with pytest.raises(_lib.RtError, match="injected"):
+            ctx.render_device(P.params(W, H, spp, 50, 6, flags=FLAG_MATERIALS), acc.data_ptr())
+        failed = ctx.sync_stats()
+        assert failed["rays"] == 0 and failed["kernel_ms"] == 0.0
+        ctx.render_device(P.params(W, H, spp, 50, 6, flags=FLAG_MATERIALS), acc.data_ptr())
+        st = ctx.sync_stats()
+        torch.cuda.synchronize()
+        ref, rays = oracle_mod.render_mat(sp, mt, lens, W, H, spp, 50, 6, threads=8)
+        assert np.array_equal(bits(acc.cpu().numpy()), bits(ref)) and st["rays"] == rays
     finally:
         ctx.close()

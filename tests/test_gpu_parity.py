@@ -154,7 +154,7 @@ def test_sampled_pixels_c3_c4(final_scene):
                 assert np.array_equal(bits(acc[0, p["i"]]), bits(unhex(p["accum"]))), p
 
 
-def test_sampled_pixels_c5_multi_chunk(final_scene, monkeypatch):
+def test_sampled_pixels_c5_multi_chunk(final_scene, knobs):
     """C5 (1200x800 at 10000 spp): the rows of 8 pixels the reference
     rendered at full spp (tests/golden/make_c5.py), on a 32 MB sample buffer
     so that each row takes 4 sample chunks whose running sums continue across
@@ -162,7 +162,7 @@ def test_sampled_pixels_c5_multi_chunk(final_scene, monkeypatch):
     fx = golden("c5_pixels.json")
     w, h, spp = fx["width"], fx["height"], fx["spp"]
     cam = np.array(unhex(fx["camera"]))
-    monkeypatch.setenv("PSRT_SAMPLE_BUF_MB", "32")  # 1200 px x 10 B: 2796-sample chunks
+    knobs("sample_buf_mb", 32)  # 1200 px x 10 B: 2796-sample chunks
     for p in fx["pixels"]:
         acc, _, st = P.render(final_scene, cam, w, h, spp, fx["max_depth"], fx["seed"],
                               row_offset=p["row"], row_stride=h)
@@ -213,15 +213,15 @@ def test_multi_chunk_large_spp(oracle_mod, tmp_path):
     w, h, spp = 64, 36, 200  # 64*36*10 B = 23 KB per sample -> 44-sample chunks of 1 MB
     want, _, _ = oracle_mod.render(sph, cam, w, h, spp, threads=8)
     code = ("import numpy as np, petershirleyraytracer_amd as P;"
+            "P.set_tuning('sample_buf_mb',1);"
             f"a,_,_=P.render(P.scene_two_spheres(),P.camera_default(),{w},{h},{spp});"
             f"np.save({str(tmp_path / 'c.npy')!r},a)")
-    env = dict(os.environ, PSRT_SAMPLE_BUF_MB="1")
-    subprocess.run([sys.executable, "-c", code], check=True, env=env, cwd=ROOT, timeout=300)
+    subprocess.run([sys.executable, "-c", code], check=True, cwd=ROOT, timeout=300)
     got = np.load(tmp_path / "c.npy")
     assert np.array_equal(bits(got), bits(want))
 
 
-def test_units_per_launch_limit(oracle_mod, monkeypatch):
+def test_units_per_launch_limit(oracle_mod, knobs):
     """A shard of more than 2^32 samples (1024 x 1024 at 4100 spp): the
     sample chunks are bounded by the 32-bit unit ids, not by the buffer, and
     balanced (2 x ~2050 samples). The frame must not depend on how the
@@ -231,9 +231,9 @@ def test_units_per_launch_limit(oracle_mod, monkeypatch):
     cam = oracle_mod.camera_default()
     w, h, spp = 1024, 1024, 4100
     assert w * h * spp > 2**32
-    monkeypatch.delenv("PSRT_SAMPLE_BUF_MB", raising=False)
+    knobs("sample_buf_mb", 49152)
     big, _, st_big = P.render(two, cam, w, h, spp)
-    monkeypatch.setenv("PSRT_SAMPLE_BUF_MB", "3000")
+    knobs("sample_buf_mb", 3000)
     small, _, st_small = P.render(two, cam, w, h, spp)
     assert np.array_equal(bits(big), bits(small))
     assert st_big["rays"] == st_small["rays"]
@@ -288,7 +288,7 @@ def test_context_device_buffers(oracle_mod):
     ctx.close()
 
 
-def test_context_repeat_renders_stats(oracle_mod, monkeypatch):
+def test_context_repeat_renders_stats(oracle_mod):
     """Renders on one context leave its queue heads and counter sets at zero
     (psrt_reduce resets them; no memset in the render's stream): repeated
     renders, RT_FLAG_NO_TAIL_PRIORITY and a multi-chunk render all give the
@@ -307,7 +307,7 @@ def test_context_repeat_renders_stats(oracle_mod, monkeypatch):
     C = FLAG_CULL_STATS
     for flags, buf_mb in ((C, None), (C, None), (C | FLAG_NO_TAIL_PRIORITY, None), (C, "1")):
         if buf_mb:
-            monkeypatch.setenv("PSRT_SAMPLE_BUF_MB", buf_mb)  # 9600 px x 10 B: 8-sample chunks
+            ctx.set_tuning("sample_buf_mb", int(buf_mb))  # 9600 px x 10 B: 8-sample chunks
         ctx.render_device(P.params(120, 80, 300, flags=flags), acc.data_ptr(), rgb.data_ptr(), s)
         st = ctx.sync_stats()
         torch.cuda.synchronize()
