@@ -319,17 +319,20 @@ def test_neighbour_lists_are_bit_identical(oracle_mod, final_scene, knobs):
 
 
 def test_far_camera_rebase_bit_exact(oracle_mod, final_scene):
-    """A camera ~1.4e10 units out (2^30 x the book's lookfrom, a field of
-    view 2^-30 of 20 degrees): every camera ray is a far origin whose
-    root-box entry, kept as a float, would move the re-based origin far
-    outside the range the FP32 slab test's error bound covers.
-    Such entries are recomputed in FP64 by the walk; the frame equals the
-    oracle's, and the counting variant sees the FP64 root-box tests."""
-    lf = tuple(np.array([13.0, 2.0, 3.0]) * 2.0 ** 30)
-    cam = P.camera_look_at(lf, (0.0, 0.5, 0.0), vfov=20.0 * 2.0 ** -30, aspect=48 / 32)
-    assert np.abs(cam[0]).max() > 1e10
+    """A camera 2^34 (1.7e10) units out on the z axis, looking back at the
+    scene through a 2e-8 degree field (about 6 units high there): every
+    camera ray is a far origin whose root-box entry, kept as a float, would
+    move the re-based origin far outside the range the FP32 slab test's
+    error bound covers. Such entries are recomputed in FP64 by
+    the walk; the frame equals the oracle's. (On the z axis the camera's
+    x / y direction components stay exact. At that range the reference's own
+    FP64 sphere test no longer resolves unit spheres, so the frame is noise;
+    what is checked is that the device reproduces it bit for bit.)"""
+    cam = P.camera_look_at((0.0, 0.5, 2.0 ** 34), (0.0, 0.5, 0.0), vfov=2e-8, aspect=48 / 32)
     a, _, sa = P.render(final_scene, cam, 48, 32, 3, seed=5, cull_stats=True)
     want, _, rays = oracle_mod.render(final_scene, cam, 48, 32, 3, seed=5, threads=8)
     assert np.array_equal(bits(a), bits(want)) and sa["rays"] == rays
-    assert sa["root_box_tests"] >= 48 * 32 * 3  # every camera ray, at least once
-    assert sa["tests_executed"] > 0 and sa["prerejects"] > 0
+    # every camera ray tests the root box in hit_quick; those that park are
+    # re-based in FP64 by the walk (counted again there)
+    samples = 48 * 32 * 3
+    assert sa["root_box_tests"] > samples and sa["box_tests"] > 0, sa
