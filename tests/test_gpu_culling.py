@@ -332,7 +332,16 @@ def test_far_camera_rebase_bit_exact(oracle_mod, final_scene):
     a, _, sa = P.render(final_scene, cam, 48, 32, 3, seed=5, cull_stats=True)
     want, _, rays = oracle_mod.render(final_scene, cam, 48, 32, 3, seed=5, threads=8)
     assert np.array_equal(bits(a), bits(want)) and sa["rays"] == rays
-    # every camera ray tests the root box in hit_quick; those that park are
-    # re-based in FP64 by the walk (counted again there)
-    samples = 48 * 32 * 3
-    assert sa["root_box_tests"] > samples and sa["box_tests"] > 0, sa
+    assert sa["root_box_tests"] >= 48 * 32 * 3, sa  # every camera ray is a far origin
+    # The walk's FP64 re-basing, ray by ray (the hittable_list::hit probe
+    # shares hit_quick and the walk): origins 2^30 .. 2^36 out, aimed at the
+    # scene without its ground (so nothing ends them before the walk),
+    # against the reference scan.
+    rng = np.random.default_rng(41)
+    n = 200_000
+    small = final_scene[1:]
+    o = rng.normal(size=(n, 3))
+    o *= (2.0 ** rng.uniform(30, 36, (n, 1))) / np.linalg.norm(o, axis=1, keepdims=True)
+    d = np.concatenate([rng.uniform(-12, 12, (n, 1)), rng.uniform(0, 2, (n, 1)),
+                        rng.uniform(-12, 12, (n, 1))], 1) - o
+    _compare(small, o, d)
