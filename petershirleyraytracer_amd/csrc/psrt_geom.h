@@ -134,10 +134,6 @@ struct GridC {
   float a0[3], a1[3];
   int top[3], pad_;
   double r_check, nb_c2;
-  // 2^44 r_check^2: a far origin's root-box entry e may be kept as a float
-  // while e^2 A <= this (hit_quick), i.e. its rounding moves the re-based
-  // origin by <= 2^-24 e |d| <= 2^-2 r_check
-  double rebase_lim;
   const uint4* plist;  // BvhView::plist (psrt_trace's camera lists), or nullptr
 };
 
@@ -155,7 +151,6 @@ __device__ __forceinline__ GridC grid_consts(const BvhView& bv) {
   g.pad_ = 0;
   g.r_check = bv.r_check;
   g.nb_c2 = bv.nb_c2;
-  g.rebase_lim = 0x1p44 * (bv.r_check * bv.r_check);
   g.plist = bv.plist;
   return g;
 }

@@ -295,8 +295,9 @@ __device__ __forceinline__ int sweep_linear(const double4* __restrict__ geo, int
 // visiting order that evaluates every sphere whose root could land in
 // [0, closest], with the same FP64 test, returns the same record. The BVH
 // (psrt_bvh.h) visits a superset: its FP32 boxes are padded past the FP32
-// slab error and the FP64 root error; rays it cannot bound (non-finite,
-// |o| > r_check, A not in (0, 1e200)) take the linear sweep.
+// slab error and the FP64 root error; rays it cannot bound (non-finite, A
+// not in (0, 1e200), |o|inf > 8 r_check) take the linear sweep; origins
+// between r_check and 8 r_check test the padded root box in FP64 first.
 
 // sphere.cc:6-31 for one sphere, then the (t, index) rule of the list scan,
 // after an exact pre-reject in FP32 (Pre32; r04, replacing r01-r03's FP64
@@ -458,7 +459,12 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
   const bool finite = (A > 0.0) && (A < 1e200);
   const double am = __builtin_fmax(__builtin_fabs(ox),
                                    __builtin_fmax(__builtin_fabs(oy), __builtin_fabs(oz)));
-  if (!finite || !(am < 1e200)) {  // unbounded arithmetic: the reference scan, verbatim
+  // Unbounded arithmetic, or an origin so far out (|o|inf > 8 r_check = 2^9 S)
+  // that the reference's own roots may err by more than the BVH pad: a root's
+  // point is good to ~1.5 x 2^-25 |o - c| near tangency, <= 2^-14.6 S (a third
+  // of the pad) for |o - c| <= 2^9.8 S. The reference scan,
+  // verbatim (NaN and infinities fail the test too).
+  if (!finite || !(am * 0.125 <= gc.r_check)) {
     cs.fp64 += n;
     bi = sweep_linear(geo, n, ox, oy, oz, dx, dy, dz, A, 0.0, __builtin_inf(), bt);
     return true;
@@ -576,11 +582,12 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
       return true;
     }
     // The walk re-bases the ray here (hit_traverse). Any nearby point of the
-    // ray serves while the float rounding of e moves it by <= 2^-24 e |d| <=
-    // r_check / 4 (then |o'| stays in the range the slab test's error bound
-    // covers, psrt_bvh.cpp); an origin farther out than that (a camera
-    // ~2^22 r_check away) gets -1: the walk recomputes the entry in FP64.
-    t0f = (e * e) * A <= gc.rebase_lim ? (float)e : -1.0f;
+    // ray serves: with |o|inf <= 2^9 S (far_lim above) the float rounding of
+    // e moves it by <= 2^-24 e |d| < 2^-14 S along the ray, and the re-based
+    // origin stays in the range the slab test's error bound covers
+    // (psrt_bvh.cpp; ADVICE r04 asked about origins beyond that range: they
+    // take the linear scan).
+    t0f = (float)e;
   }
   clk.util(kUPark);
   return false;
@@ -596,19 +603,6 @@ __device__ __forceinline__ void hit_traverse(const BvhView& bv, const float4* __
                                              double ox, double oy, double oz, double dx, double dy,
                                              double dz, double A, double& bt, int& bi,
                                              CS& cs, int& node, unsigned tail, double t0) {
-  // t0 < 0: an origin too far out for a float entry (hit_quick): the entry
-  // in FP64, for the current bt; a segment that now misses the root box
-  // (bt shrank in an earlier pass) can improve on nothing: the walk is over
-  if (__builtin_expect(__ballot(t0 < 0.0) != 0, 0)) {
-    if (t0 < 0.0) {
-      ++cs.root;
-      t0 = root_box_entry(bv, ox, oy, oz, dx, dy, dz, bt);
-      if (t0 < 0.0) {
-        t0 = 0.0;
-        node = bv.n_nodes;
-      }
-    }
-  }
   // Far origins are re-based at their root-box entry o' = o + t0 d (FP64), so
   // the FP32 slab test sees |o'| <= the scene scale and its error bound holds;
   // box intervals are then tested over [-t0, bt - t0]. The exact sphere tests

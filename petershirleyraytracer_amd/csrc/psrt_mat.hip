@@ -121,8 +121,10 @@ __device__ __forceinline__ bool hit_quick_m(TestCount<kCount>& nt, TestCount<kCo
   bi = -1;
   const double am = __builtin_fmax(__builtin_fabs(ox),
                                    __builtin_fmax(__builtin_fabs(oy), __builtin_fabs(oz)));
-  // unbounded arithmetic or no BVH: the reference scan, verbatim
-  if (!kBVH || !(A > 0.0 && A < 1e200) || !(am < 1e200)) {
+  // unbounded arithmetic, no BVH, or an origin beyond 2^9 S (where the
+  // reference's roots may err by more than the pad, psrt_trace hit_quick):
+  // the reference scan, verbatim
+  if (!kBVH || !(A > 0.0 && A < 1e200) || !(am * 0.125 <= gc.r_check)) {
     for (int i = 0; i < n; ++i) test_sphere_m(geo[i], i, ox, oy, oz, dx, dy, dz, A, bt, bi);
     nt.add((unsigned)n);
     return true;
