@@ -132,6 +132,9 @@ def parse():
     ap.add_argument("--scaling", default="strong", choices=("weak", "strong"),
                     help="strong (default): the configured frame on any N; weak (study): "
                          "N GPUs render the frame at N x spp (per-GPU work fixed)")
+    ap.add_argument("--tune", default="",
+                    help="measurement knobs (include/rt.h rt_context_set_tuning), name=value[,...]; "
+                         "every knob keeps the output bit-identical")
     ap.add_argument("--emulate-shard", default="",
                     help="R/G: one process renders only rank R's rows of a G-GPU run "
                          "(per-rank step time of the multi-GPU bench, on one GPU; "
@@ -395,6 +398,9 @@ def main():
         else:
             dist.init_process_group(backend)
 
+    for kv in filter(None, args.tune.split(",")):  # process defaults: every context takes them
+        name, val = kv.split("=")
+        P.set_tuning(name.strip(), float(val))
     w, h, spp = cfg["width"], cfg["height"], cfg["spp"]
     spheres, cam = scene_of(cfg)
     config_id = args.config
@@ -769,7 +775,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic (procedural scene: final random-spheres, glibc srand(1); counter RNG seed 0)",
             "config": {"workload": cfg["desc"] + (f"; {n_shards} GPUs at {n_shards} x spp (weak scaling: {cfg['spp']} spp of work per GPU)" if args.scaling == "weak" and n_shards > 1 else ""),
-                       "config_id": config_id, "width": w,
+                       "config_id": config_id, "width": w, **({"tune": args.tune} if args.tune else {}),
                        "height": h, "spp": spp, "max_depth": args.max_depth, "spheres": n,
                        "parallelism": (f"emulated shard {args.emulate_shard} (rows {off}::{stride})"
                                        if args.emulate_shard else f"interleaved rows x{world}") + ((", RCCL FP64 framebuffer gather" if args.gather_fp64 else ", per-rank write_color + RCCL uint8 gather") if world > 1 else "")},
