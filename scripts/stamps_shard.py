@@ -1,4 +1,4 @@
-"""Diagnostic (PSRT_STAMPS build): the wave timeline (start, queue-empty and
+"""Diagnostic (the stamps tuning knob): the wave timeline (start, queue-empty and
 exit times over waves) of a C3 shard launch of 1 and of 20 frames.
 
   python3 scripts/stamps_shard.py R G
@@ -22,7 +22,7 @@ ptr = [acc[f].data_ptr() for f in range(20)]
 for nb in (1, 20, 1, 20):
     ctx.render_device_frames(prm, nb, ptr[:nb], None, s)
     ctx.sync_stats()
-os.environ["PSRT_STAMPS"] = "1"
+ctx.set_tuning("stamps", 1)  # the diagnostic kernel variant (include/rt.h tuning knobs)
 for nb in (1, 20):
     ctx.render_device_frames(prm, nb, ptr[:nb], None, s)
     st = ctx.sync_stats()
