@@ -103,7 +103,6 @@ struct Tuning {
   double stamps = 0;         // diagnostic kernel variant (section clocks, utilisation probes)
   double scene_rebuild = 0;  // rebuild the culling structures for an unchanged scene
   double big_ratio = 0;      // radius ratio of the big-sphere class (0: psrt_bvh's default)
-  double no_escape = 0;      // 1: no escape table: unbounded rays walk the BVH
 };
 }  // namespace psrt
 
@@ -121,7 +120,7 @@ const TuningKey kTuningKeys[] = {
     {"blocks_per_cu", &psrt::Tuning::blocks_per_cu}, {"mat_lds", &psrt::Tuning::mat_lds},
     {"mat_batch", &psrt::Tuning::mat_batch},         {"flush_at", &psrt::Tuning::flush_at},
     {"stamps", &psrt::Tuning::stamps},               {"scene_rebuild", &psrt::Tuning::scene_rebuild},
-    {"big_ratio", &psrt::Tuning::big_ratio},         {"no_escape", &psrt::Tuning::no_escape},
+    {"big_ratio", &psrt::Tuning::big_ratio},
 };
 std::mutex g_tuning_mu;
 psrt::Tuning g_tuning;  // the process defaults (rt_context_set_tuning(NULL, ...))
@@ -156,7 +155,6 @@ struct rt_context {
   int* d_nb_items = nullptr;
   uint4* d_cell_rec = nullptr;  // grid lists as inline records (BvhHost::cell_rec)
   uint2* d_nb_rec = nullptr;    // neighbour lists as inline records (BvhHost::nb_rec)
-  unsigned* d_esc = nullptr;    // escape table (psrt_escape_table), [n][kEscWords]
   std::vector<rt_sphere> scene;   // the scene the structures were built for
   psrt::GridHost pgrid;  // point-location grid (host copy of the geometry)
   double pad = 0.0;
@@ -397,7 +395,6 @@ int rt_context_destroy(rt_context* c) {
   (void)hipFree(c->d_nb_items);
   (void)hipFree(c->d_cell_rec);
   (void)hipFree(c->d_nb_rec);
-  (void)hipFree(c->d_esc);
   (void)hipFree(c->d_mats);
   (void)hipFree(c->d_path);
   for (auto e : c->ev) (void)hipEventDestroy(e);
@@ -495,8 +492,6 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
   (void)hipFree(c->d_nb_items);
   (void)hipFree(c->d_cell_rec);
   (void)hipFree(c->d_nb_rec);
-  (void)hipFree(c->d_esc);
-  c->d_esc = nullptr;
   c->d_nodes = nullptr, c->d_leaf_geo = nullptr, c->d_leaf_idx = nullptr, c->d_big = nullptr;
   c->d_cell_start = nullptr, c->d_cell_items = nullptr;
   c->d_nb_word = nullptr, c->d_nb_items = nullptr;
@@ -550,23 +545,6 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
       HIP_TRY(up(c->d_cell_rec, b.cell_rec.data(), b.cell_rec.size() * sizeof(uint32_t)));
     if (!b.nb_rec.empty())
       HIP_TRY(up(c->d_nb_rec, b.nb_rec.data(), b.nb_rec.size() * sizeof(uint32_t)));
-    // the escape table: one block per BVH sphere, on the
-    // device; it depends on the spheres only (not the camera)
-    if (c->n_leaf > 0 && n < (int)psrt::kCamOverflow) {
-      const size_t words = (size_t)n * psrt::kEscWords;
-      HIP_TRY(hipMalloc(&c->d_esc, words * sizeof(unsigned)));
-      HIP_TRY(hipMemsetAsync(c->d_esc, 0, words * sizeof(unsigned), c->stream));
-      psrt::EscArgs ea{};
-      ea.geo = c->d_geo;
-      ea.leaf_idx = c->d_leaf_idx;
-      ea.n_leaf = c->n_leaf;
-      ea.nb_rec = c->d_nb_rec;
-      ea.pad = b.pad;
-      ea.table = c->d_esc;
-      hipLaunchKernelGGL(psrt::psrt_escape_table, dim3(c->n_leaf), dim3(psrt::kEscBins), 0,
-                         c->stream, ea);
-      HIP_TRY(hipGetLastError());
-    }
     // the uploads above read host vectors of this block: wait for them here
     HIP_TRY(hipStreamSynchronize(c->stream));
   }
@@ -598,7 +576,6 @@ static psrt::BvhView bvh_view(const rt_context* c) {
   v.nb_rec = c->d_nb_rec;
   v.nb_c2 = 0.25 * c->pad * c->pad;
   if (c->tune.no_neighbors) v.nb_c2 = -1.0;  // C^2 <= -r^2 never holds
-  v.esc = c->tune.no_escape ? nullptr : c->d_esc;
   // grid bounds / scale in FP32, as used: the cell index of the device is a
   // function of these exact float values, and the host places each sphere in
   // every cell its padded box overlaps under the SAME float cell boundaries
@@ -1261,15 +1238,15 @@ int rt_context_sync_stats(rt_context* c, rt_stats* s) {
   c->last.kernel_ms = kms;
   c->last.total_ms = all;
   if (c->last_stamps) {  // the diagnostic variant's section clocks and probes
-    unsigned long long sec[62];
+    unsigned long long sec[60];
     HIP_TRY(hipMemcpy(sec, c->d_counters + 8, sizeof sec, hipMemcpyDeviceToHost));
-    static const char* names[25] = {"refill", "store", "hit", "hint", "nb", "cam",
+    static const char* names[24] = {"refill", "store", "hit", "hint", "nb", "cam",
                                     "grid", "walk", "trial", "scatter", "hint_hit",
                                     "hint_tiny", "grid_cell", "grid_out", "grid_none_fin",
-                                    "grid_none_inf", "far_miss", "park", "list_trip", "escape",
+                                    "grid_none_inf", "far_miss", "park", "list_trip",
                                     "walk_bvh", "walk_big", "walk_miss", "walk_fin", "walk_inf"};
     std::string u = "{\"psrt_util\": {";
-    for (int k = 0; k < 25; ++k) {
+    for (int k = 0; k < 24; ++k) {
       char b[128];
       const double w = (double)sec[12 + 2 * k], l = (double)sec[13 + 2 * k];
       std::snprintf(b, sizeof b, "%s\"%s\": [%.4g, %.2f]", k ? ", " : "", names[k], w,

@@ -135,7 +135,6 @@ struct GridC {
   int top[3], pad_;
   double r_check, nb_c2;
   const uint4* plist;  // BvhView::plist (psrt_trace's camera lists), or nullptr
-  const unsigned* esc;  // BvhView::esc (the escape table), or nullptr
 };
 
 __device__ __forceinline__ GridC grid_consts(const BvhView& bv) {
@@ -153,31 +152,9 @@ __device__ __forceinline__ GridC grid_consts(const BvhView& bv) {
   g.r_check = bv.r_check;
   g.nb_c2 = bv.nb_c2;
   g.plist = bv.plist;
-  g.esc = bv.esc;
   return g;
 }
 
-
-// Cube-map bin of a direction (FP32; the escape table's cones are widened
-// by 1e-5 rad, far beyond this rounding): face = the axis of the largest |d_k|
-// (ties to the lower axis) and its sign; cell (i, j) of the other two
-// coordinates, each over that one, kEscN x kEscN per face. psrt_escape_table
-// builds the cone of bin ((2 face + neg) kEscN + j) kEscN + i to match.
-__device__ __forceinline__ int esc_bin(float x, float y, float z) {
-  const float ax = __builtin_fabsf(x), ay = __builtin_fabsf(y), az = __builtin_fabsf(z);
-  const bool fx = ax >= ay && ax >= az;
-  const bool fy = !fx && ay >= az;
-  const float m = fx ? ax : (fy ? ay : az);
-  const float u = fx ? y : x;              // face x: (y, z); y: (x, z); z: (x, y)
-  const float v = fx ? z : (fy ? z : y);
-  const float w = fx ? x : (fy ? y : z);
-  const float h = 0.5f * kEscN;
-  const float k = h * __builtin_amdgcn_rcpf(m);
-  const int i = min(kEscN - 1, max(0, (int)__builtin_floorf(__builtin_fmaf(u, k, h))));
-  const int j = min(kEscN - 1, max(0, (int)__builtin_floorf(__builtin_fmaf(v, k, h))));
-  const int face = 2 * (fx ? 0 : (fy ? 1 : 2)) + (w < 0.0f ? 1 : 0);
-  return (face * kEscN + j) * kEscN + i;
-}
 
 // floor(x) as int, saturating (NaN -> 0): one v_cvt_flr_i32_f32
 __device__ __forceinline__ int cvt_flr_i32(float x) {

@@ -158,25 +158,6 @@ struct BvhView {
   // 2^-60 rounded up (+inf beyond 2^40): the FP32 pre-reject (psrt_kernels.hip
   // Pre32) of test_sphere
   const float4* __restrict__ geo32;    // [n]
-  // escape table (psrt_escape_table), or nullptr: per sphere j,
-  // kEscBins bits, bit b set when no BVH sphere outside j's neighbour list
-  // can be hit by a ray leaving j's surface in a direction of cube-map bin b
-  const unsigned* __restrict__ esc;    // [n][kEscWords]
-};
-
-// Escape table geometry: a cube map of kEscN x kEscN bins per face.
-constexpr int kEscN = 8;
-constexpr int kEscBins = 6 * kEscN * kEscN;
-constexpr int kEscWords = kEscBins / 32;
-static_assert(kEscBins % 64 == 0, "one wave per 64 bins in psrt_escape_table");
-
-struct EscArgs {
-  const double4* __restrict__ geo;    // {c, r*r} by sphere index
-  const int* __restrict__ leaf_idx;   // BVH spheres (original indices)
-  int n_leaf;
-  const uint2* __restrict__ nb_rec;   // neighbour records by sphere index
-  double pad;                         // BVH box padding (absolute)
-  unsigned* __restrict__ table;       // [n][kEscWords], zeroed by the host
 };
 
 constexpr int kCamTile = 8;         // camera-list tiles are 8 x 8 pixels (one wave)
@@ -325,7 +306,6 @@ __global__ void psrt_trace(const double4* __restrict__ geo, const double* __rest
                            double* __restrict__ samples, TraceArgs a, BvhView bv);
 __global__ void psrt_reduce(ReduceArgs a);
 __global__ void psrt_camera_lists(CamListArgs a);
-__global__ void psrt_escape_table(EscArgs a);
 __global__ void psrt_quantize(const double* __restrict__ accum, unsigned char* __restrict__ rgb8,
                               unsigned n, int spp);
 __global__ void psrt_probe_hit(const double4* __restrict__ geo, const double* __restrict__ inv_r,

@@ -92,7 +92,7 @@ enum Util { kURefill = 0, kUStore, kUHit, kUHint, kUNb, kUCam, kUGrid, kUWalk, k
             kUScatter,
             // hit_quick outcomes (lanes per wave execution, counted where decided)
             kUHintHit, kUHintTiny, kUGridCell, kUGridOut, kUGridNoneFin, kUGridNoneInf,
-            kUFarMiss, kUPark, kUListTrip, kUEscape,
+            kUFarMiss, kUPark, kUListTrip,
             // walk outcomes: {rays, summed box tests} by result (BVH sphere / big / none)
             // and by whether the ray parked with a finite bound
             kUWBvh, kUWBig, kUWMiss, kUWFin, kUWInf, kUCount };
@@ -471,7 +471,6 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
   }
   const Pre32 pr = pre32_of(ox, oy, oz, A, am);
   bool fix = false, full = false, nb = false;
-  unsigned esc_w = 0u, esc_bit = 0u;  // escape table word and this ray's bin bit
   // The candidate list as an inline record {count | i0 << 16, i1 | i2 << 16,
   // ...} (uint16 slots, count kListOverflow = none): a camera ray's pixel list
   // (psrt_camera_lists), loaded early; the hint sphere's neighbour record or
@@ -497,19 +496,11 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     // to ~2^-19 S) stays in that ball. A sphere with an accepted root t <= bt
     // has its hit point there and within the root error of its own surface,
     // so its centre lies within r_j + r_k + pad of c_j: it is j's neighbour.
-    const bool near = am <= gc.r_check && gc.nb_c2 >= 0.0 &&
-                      (ch <= 0.0 || ch * ch <= gc.nb_c2 * sh.w);
-    if (bi == hint && near) {
+    if (bi == hint && am <= gc.r_check && gc.nb_c2 >= 0.0 &&
+        (ch <= 0.0 || ch * ch <= gc.nb_c2 * sh.w)) {
       const uint2 nr = sv.nb(hint);
       nb = (nr.x & 0xFFFFu) != kCamOverflow;
       if (nb) rec = make_uint4(nr.x, nr.y, 0u, 0u);
-    } else if (bi < 0 && near && gc.esc && pr.sk < __builtin_inff()) {
-      // Escape path: j not re-hit, the origin within pad/4
-      // of j's surface. The table word of (j, bin(d)) is loaded now, used
-      // after the big spheres (if they leave the ray unbounded too).
-      const int b = esc_bin((float)dx, (float)dy, (float)dz);
-      esc_w = gc.esc[hint * kEscWords + (b >> 5)];
-      esc_bit = 1u << (b & 31);
     }
   }
   clk.mark(kSecQHint);
@@ -526,21 +517,9 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
     }
   }
   clk.mark(kSecQBig);
-  // Escape path: still unbounded after j and the big
-  // spheres, and the table proves no BVH sphere outside j's neighbour list
-  // can be hit from j's surface in this direction bin: j's neighbour list is
-  // the ray's candidate list, as on the nb path.
-  if (bi < 0 && (esc_w & esc_bit) != 0u) {
-    const uint2 nr = sv.nb(hint);
-    if ((nr.x & 0xFFFFu) != kCamOverflow) {
-      clk.util(kUEscape);
-      nb = true;
-      rec = make_uint4(nr.x, nr.y, 0u, 0u);
-    }
-  }
   // The candidate list of this ray, one of:
-  //   neighbour list of the hint sphere (nb path; also the escape path), the
-  //   pixel's camera list, or the grid cell holding [o, o + bt d];
+  //   neighbour list of the hint sphere (nb path), the pixel's camera list,
+  //   or the grid cell holding [o, o + bt d];
   // all three are records of the same form, walked by ONE loop below, so a
   // wave whose lanes took different paths runs max(count) sphere tests
   // instead of their sum, and no trip loads anything but the sphere.
@@ -1501,74 +1480,6 @@ __global__ __launch_bounds__(64) void psrt_camera_lists(CamListArgs a) {
     if (!full) w[0] = (w[0] & 0xFFFF0000u) | n;
   }
   a.plist[(size_t)rk * a.width + px] = make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-// ---- escape table -----------------------------------------
-//
-// Bit b of sphere j: no BVH sphere k outside j's neighbour list (and not j)
-// can return an accepted root to a ray leaving j's surface (origin within
-// pad/4 of it) in a direction of cube-map bin b. Such a root puts the hit
-// point within the root error (<< pad, |o| <= r_check) of k's surface, so
-// the half-line from c_j in the ray's direction passes within
-// R = |r_j| + |r_k| + 1.5 pad of c_k (the origin is within |r_j| + pad/4 of
-// c_j): the bin's cone (apex c_j, widened by 1e-5 rad, far above the FP32
-// binning error of esc_bin) must meet ball(c_k, R), widened by 2^-20 as the
-// camera lists' test (cone_meets). Non-neighbours lie farther than R from
-// c_j, so the apex is outside every ball tested. Rows of spheres whose
-// neighbour list does not fit a record stay zero. One block per BVH sphere,
-// one thread per bin.
-__global__ __launch_bounds__(kEscBins) void psrt_escape_table(EscArgs a) {
-  const int j = a.leaf_idx[blockIdx.x];
-  const uint2 nr = a.nb_rec[j];
-  const unsigned cnt = nr.x & 0xFFFFu;
-  if (cnt == kCamOverflow) return;  // block-uniform
-  const int n1 = cnt > 0 ? (int)(nr.x >> 16) : -1, n2 = cnt > 1 ? (int)(nr.y & 0xFFFFu) : -1,
-            n3 = cnt > 2 ? (int)(nr.y >> 16) : -1;
-  const int b = threadIdx.x;
-  const int face = b / (kEscN * kEscN), cj = (b / kEscN) % kEscN, ci = b % kEscN;
-  const int f = face >> 1, uo = f == 0 ? 1 : 0, vo = f == 2 ? 1 : 2;
-  const double sg = (face & 1) ? -1.0 : 1.0;
-  // bin directions: d[f] = sg, d[uo] = s, d[vo] = t (esc_bin's face axes)
-  auto dir = [&](double s, double t, double d[3]) {
-    d[f] = sg, d[uo] = s, d[vo] = t;
-    const double il = 1.0 / __builtin_sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
-    d[0] *= il, d[1] *= il, d[2] *= il;
-  };
-  const double step = 2.0 / kEscN;
-  const double s0 = -1.0 + ci * step, s1 = s0 + step, t0 = -1.0 + cj * step, t1 = t0 + step;
-  Cone c;
-  double ax[3], d[3];
-  dir(0.5 * (s0 + s1), 0.5 * (t0 + t1), ax);
-  c.ax = ax[0], c.ay = ax[1], c.az = ax[2];
-  double cmin = 1.0;
-  const double ss[2] = {s0, s1}, ts[2] = {t0, t1};
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {  // the bin is a planar quadrilateral on the face:
-    dir(ss[e & 1], ts[e >> 1], d);  // the largest angle to the axis is at a corner
-    cmin = __builtin_fmin(cmin, (ax[0] * d[0] + ax[1] * d[1]) + ax[2] * d[2]);
-  }
-  c.ca = cmin - 1e-5;  // cos(alpha + delta) >= cos(alpha) - delta
-  c.sa = __builtin_sqrt(__builtin_fmax(0.0, 1.0 - c.ca * c.ca));
-  c.ok = true;
-  const double4 g = a.geo[j];
-  const double rj = __builtin_sqrt(g.w);
-  CamListArgs apex{};  // cone_meets reads the apex from org
-  apex.org[0] = g.x, apex.org[1] = g.y, apex.org[2] = g.z;
-  apex.pad = 0.0;
-  bool empty = true;
-  for (int e = 0; e < a.n_leaf && empty; ++e) {
-    const int k = a.leaf_idx[e];
-    if (k == j || k == n1 || k == n2 || k == n3) continue;
-    const double4 q = a.geo[k];
-    // ball(c_k, R): cone_meets widens sqrt(w) + pad by 2^-20
-    const double R = rj + __builtin_sqrt(q.w) + 1.5 * a.pad;
-    empty = !cone_meets(c, apex, make_double4(q.x, q.y, q.z, R * R));
-  }
-  const uint64_t m = __ballot(empty);
-  const unsigned lane = __lane_id();
-  unsigned* const row = a.table + (size_t)j * kEscWords;
-  if (lane == 0) row[b / 32] = (unsigned)m;
-  if (lane == 32) row[b / 32] = (unsigned)(m >> 32);
 }
 
 __global__ __launch_bounds__(256) void psrt_quantize(const double* __restrict__ accum,
