@@ -891,8 +891,13 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
           kk = (unsigned short)(k < kSampleKCap ? k : kSampleKCap);
         }
         const unsigned u = su;  // < total < 2^32
+#if PSRT_TEMPORAL_RECORDS  // measurement build (write-traffic A/B, profiles/r05_writes)
+        samples[u] = tt;
+        ((unsigned short*)(samples + total))[u] = kk;
+#else
         __builtin_nontemporal_store(tt, samples + u);
         __builtin_nontemporal_store(kk, (unsigned short*)(samples + total) + u);
+#endif
         done = false;
       }
     }

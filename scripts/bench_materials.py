@@ -3,9 +3,14 @@
 W x H x spp, max depth 50, on one GPU, with the C restatement timed on the
 host cores beside it (a bounded sample of rows).
 
-    python scripts/bench_materials.py [--width 1200 --height 800 --spp 10 --steps 3]
+    python scripts/bench_materials.py [--width 1200 --height 800 --spp 10 --steps 10]
 
 Prints one JSON line. Frames are device-resident (no D2H in the timed region).
+`value` is the rate of the timed frames in launches of --batch frames
+(rt_render_device_frames; 0 = auto: all timed frames in one launch, <= 32),
+as bench.py's headline; `unbatched` is the same frames one per launch. The
+roofline counts what the counting variant executed, with bench.py's issue
+weights (WEIGHTS: measured instruction costs, scripts/isa_rates.hip).
 """
 import argparse
 import json
@@ -28,6 +33,8 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=8)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cull", action="store_true")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="frames per trace launch (<= 32; 0 = all timed frames, 1 = one per launch)")
     a = ap.parse_args()
 
     import torch
@@ -44,37 +51,62 @@ def main():
     rgb = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
     flags = FLAG_MATERIALS | (FLAG_NO_CULL if a.no_cull else 0)
     st = ctx.stream()
+    B = min(32, a.steps) if a.batch <= 0 else min(32, a.batch)
+    accs = [torch.zeros((H, W, 3), dtype=torch.float64, device="cuda") for _ in range(max(1, B))]
     for i in range(a.warmup):
         ctx.render_device(P.params(W, H, S, a.depth, 100 + i, flags=flags), acc.data_ptr(),
                           rgb.data_ptr(), st)
         ctx.sync_stats()
-    ms, kms, rays = [], [], 0
-    for i in range(a.steps):
+    if B > 1:  # the sample buffer grows to B frames outside the timed region
+        ctx.render_device_frames(P.params(W, H, S, a.depth, 200, flags=flags), B,
+                                 [x.data_ptr() for x in accs], None, st)
+        ctx.sync_stats()
+
+    def timed(b):
+        """a.steps frames (seeds 0..) in launches of up to b frames"""
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        ctx.render_device(P.params(W, H, S, a.depth, i, flags=flags), acc.data_ptr(),
-                          rgb.data_ptr(), st)
-        s = ctx.sync_stats()
-        ms.append((time.perf_counter() - t0) * 1e3)
-        kms.append(s["kernel_ms"])
-        rays += s["rays"]
-    step = sum(ms) / len(ms)
+        kms, rays, f0 = 0.0, 0, 0
+        while f0 < a.steps:
+            nb = min(b, a.steps - f0)
+            if nb == 1:
+                ctx.render_device(P.params(W, H, S, a.depth, f0, flags=flags), acc.data_ptr(),
+                                  rgb.data_ptr(), st)
+            else:
+                ctx.render_device_frames(P.params(W, H, S, a.depth, f0, flags=flags), nb,
+                                         [x.data_ptr() for x in accs[:nb]], None, st)
+            s = ctx.sync_stats()
+            kms += s["kernel_ms"]
+            rays += s["rays"]
+            f0 += nb
+        return (time.perf_counter() - t0) * 1e3 / a.steps, kms / a.steps, rays
+
+    step, kms, rays = timed(B)
+    unbatched = None
+    if B > 1:
+        s1, k1, _ = timed(1)
+        unbatched = {"ms_per_step": round(s1, 4), "value": round(W * H * S / (s1 * 1e3), 2),
+                     "kernel_ms": round(k1, 4)}
     # one untimed frame of the counting variant: the sphere / box tests the
     # kernel executes (deterministic: the same for every frame of a seed)
     ctx.render_device(P.params(W, H, S, a.depth, 0, flags=flags | FLAG_CULL_STATS),
                       acc.data_ptr(), rgb.data_ptr(), st)
     cs = ctx.sync_stats()
-    kms = sum(kms) / len(kms)
-    # FP64-op slots as bench.py counts them for psrt_trace: 18 per exact sphere
-    # test, 7 per FP32 box test, ~61 per traced ray (hit record, scatter, draws)
-    ops = cs["tests_executed"] * 18 + cs["box_tests"] * 7 + cs["rays"] * 61
+    # FP64-op slots as bench.py counts them for psrt_trace (WEIGHTS: every
+    # sphere test of this kernel is a full FP64 one, there is no pre-reject)
+    from bench import SHADE_OPS_PER_RAY, WEIGHTS
+    ops = (cs["tests_executed"] * WEIGHTS["full_sphere_test"] + cs["box_tests"] * WEIGHTS["box_test"]
+           + cs["root_box_tests"] * WEIGHTS["root_box_test"] + cs["rays"] * SHADE_OPS_PER_RAY)
     achieved = ops / (kms * 1e-3) / 1e12
     roof = {"bound": "valu", "achieved": round(achieved, 4), "peak": 39.32, "unit": "TFLOP/s",
             "frac": round(achieved / 39.32, 4), "traffic": None, "kernel": "psrt_trace_mat",
-            "avg_launch_ms": round(kms, 4), "executed_sphere_tests_per_launch": cs["tests_executed"],
-            "executed_box_tests_per_launch": cs["box_tests"], "rays_per_launch": cs["rays"],
-            "note": "FP64-op slots (tests x 18 + boxes x 7 + rays x 61) / kernel time, "
-                    "against 256 CU x 64 lanes x 2.4 GHz non-FMA FP64"}
+            "avg_launch_ms": round(kms, 4), "full_sphere_tests_per_launch": cs["tests_executed"],
+            "box_tests_evaluated_per_launch": cs["box_tests"],
+            "root_box_tests_per_launch": cs["root_box_tests"], "rays_per_launch": cs["rays"],
+            "issue_weights_fp64_slots": {k: round(v, 3) for k, v in WEIGHTS.items()},
+            "note": "FP64-op slots (full FP64 sphere tests, FP32 slab tests and FP64 root-box "
+                    "tests executed, each x its issue weight, + rays x 61) / kernel time per "
+                    "frame, against 256 CU x 64 lanes x 2.4 GHz non-FMA FP64"}
     pmc = os.path.join(ROOT, "profiles", "pmc_mat.json")
     if os.path.exists(pmc):
         d = json.load(open(pmc))
@@ -93,12 +125,13 @@ def main():
         "unit": "Msamples/s",
         "ms_per_step": step,
         "kernel_ms": kms,
-        "grays_per_s": rays / (sum(ms) * 1e6),
+        "grays_per_s": rays / (step * a.steps * 1e6),
         "rays_per_sample": rays / (a.steps * W * H * S),
         "config": {"scene": "book_final(seed 1), 487 spheres, lambertian/metal/dielectric",
                    "width": W, "height": H, "spp": S, "max_depth": a.depth,
                    "lens": "aperture 0.1, focus 10", "cull": not a.no_cull},
         "steps": a.steps, "warmup": a.warmup, "dtype": "f64", "roofline": roof,
+        "frames_per_launch": B, "unbatched": unbatched,
     }
     ctx.close()
     # the C restatement on the host cores (the usable ones: affinity capped by

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 DST=${1:-profiles/mat}
 OUT=gpurun_out/prof_mat
 mkdir -p $OUT
-B="scripts/bench_materials.py --spp 10 --cpu-rows 1"
+B="scripts/bench_materials.py --spp 10 --cpu-rows 1 --batch 1"  # one frame per dispatch
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $B > $OUT/trace.log 2>&1
 rc=$?; echo "mat trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 for pmc in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
