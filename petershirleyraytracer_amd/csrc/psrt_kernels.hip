@@ -582,7 +582,7 @@ __device__ __forceinline__ bool hit_quick(const double4* __restrict__ geo,
       return true;
     }
     // The walk re-bases the ray here (hit_traverse). Any nearby point of the
-    // ray serves: with |o|inf <= 2^9 S (far_lim above) the float rounding of
+    // ray serves: with |o|inf <= 2^9 S (the 8 r_check guard above) the float rounding of
     // e moves it by <= 2^-24 e |d| < 2^-14 S along the ray, and the re-based
     // origin stays in the range the slab test's error bound covers
     // (psrt_bvh.cpp; ADVICE r04 asked about origins beyond that range: they

@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 DST=${1:-profiles/mat}
-OUT=gpurun_out/prof_mat
+OUT=${OUTDIR:-gpurun_out/prof_mat}
 mkdir -p $OUT
 B="scripts/bench_materials.py --spp 10 --cpu-rows 1 --batch 1"  # one frame per dispatch
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $B > $OUT/trace.log 2>&1

@@ -11,7 +11,7 @@ decided by testing those. Rays from the ground (a big sphere) use a table
 per 2-D grid column of the ground instead (apex box: the column's ground
 patch). Analysis only; prints the catch rates.
 
-    python scripts/escape_model.py [samples] [N bins per cube face edge]
+    python tests/models/escape_model.py [samples] [N bins per cube face edge]
 """
 import math
 import os
@@ -19,7 +19,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import oracle  # noqa: E402
 

@@ -1,7 +1,7 @@
 /* Ray-mix statistics of C3 (final scene, 1200x800, depth 50) from the C oracle:
  * classes of the traced rays (the device ends a sample at its first C == 0
  * origin). Analysis only.
- *   gcc -O2 -ffp-contract=off -Ioracle -o /tmp/raymix scripts/raymix.c -lm -lpthread && /tmp/raymix 20000 */
+ *   gcc -O2 -ffp-contract=off -Ioracle -o /tmp/raymix tests/models/raymix.c -lm -lpthread && /tmp/raymix 20000 */
 #include "../oracle/rt_oracle.c"
 #include <stdio.h>
 static double Cof(const rt_sphere* s, const double o[3]) {
