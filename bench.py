@@ -358,8 +358,8 @@ def profile_counters(config: str):
             valu["valu_pipe_busy_mix"] = round((4 * f64 + 2 * (c["SQ_INSTS_VALU"] - f64))
                                                / simd_cycles, 4)
         if "SQ_THREAD_CYCLES_VALU" in c and "SQ_ACTIVE_INST_VALU" in c:
-            # lanes active per VALU instruction (SIMT divergence): thread-cycles /
-            # (64 x instruction quad-cycles x 4)
+            # lanes active per VALU instruction (SIMT divergence), as rocprof's
+            # VALUUtilization: SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU)
             valu["lane_utilisation"] = round(c["SQ_THREAD_CYCLES_VALU"]
                                              / (64.0 * c["SQ_ACTIVE_INST_VALU"]), 4)
     except Exception:
