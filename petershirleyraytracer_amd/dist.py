@@ -50,6 +50,13 @@ def gather_frames(local: torch.Tensor, height: int, rank: int, world: int,
     sends an all-padding block. The destination then de-interleaves."""
     if world == 1:
         return local
+    return _gather_blocks(local, height, rank, world, dst)
+
+
+def _gather_blocks(local: torch.Tensor, height: int, rank: int, world: int,
+                   dst: int) -> Optional[torch.Tensor]:
+    """The collective of `gather_frames` (also run at world 1 by the GPU test
+    that drives RCCL's gather on device frames on a one-GPU box)."""
     max_rows = rows_owned(height, 0, world)
     mine = rows_owned(height, rank, world)
     if local.dim() != 4 or local.shape[1] != mine:
