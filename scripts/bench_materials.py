@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=8)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cull", action="store_true")
+    ap.add_argument("--tune", default="",
+                    help="measurement knobs (include/rt.h rt_context_set_tuning), name=value[,...]")
     ap.add_argument("--batch", type=int, default=0,
                     help="frames per trace launch (<= 32; 0 = all timed frames, 1 = one per launch)")
     a = ap.parse_args()
@@ -41,6 +43,9 @@ def main():
     import petershirleyraytracer_amd as P
     from petershirleyraytracer_amd.render import FLAG_CULL_STATS, FLAG_MATERIALS, FLAG_NO_CULL
 
+    for kv in filter(None, a.tune.split(",")):
+        k, v = kv.split("=")
+        P.set_tuning(k.strip(), float(v))
     W, H, S = a.width, a.height, a.spp
     sp, mt = P.scene_book_final(1)
     lens = P.camera_look_at_lens(aspect=W / H)
@@ -129,7 +134,8 @@ def main():
         "rays_per_sample": rays / (a.steps * W * H * S),
         "config": {"scene": "book_final(seed 1), 487 spheres, lambertian/metal/dielectric",
                    "width": W, "height": H, "spp": S, "max_depth": a.depth,
-                   "lens": "aperture 0.1, focus 10", "cull": not a.no_cull},
+                   "lens": "aperture 0.1, focus 10", "cull": not a.no_cull,
+                   **({"tune": a.tune} if a.tune else {})},
         "steps": a.steps, "warmup": a.warmup, "dtype": "f64", "roofline": roof,
         "frames_per_launch": B, "unbatched": unbatched,
     }

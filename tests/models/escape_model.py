@@ -135,6 +135,26 @@ def main():
             gtable[key] = ok
         return gtable[key]
 
+    # direction lists (r05, the material kernel's MatArgs::dl): every BVH sphere
+    # the (key, bin) cone meets, up to 7, else overflow; keys: the hint sphere
+    # j (apex c_j, widened by |r_j| + pad) or the 3-D cell (edge g) of a
+    # ground origin (apex the cell centre, widened by half its diagonal)
+    lists = {}
+
+    def dlist(key, b, apex, wid):
+        if (key, b) not in lists:
+            L = []
+            for k in bvh:
+                if isinstance(key, int) and k == key:
+                    continue
+                if cone_meets(axes[b], ca[b], sa[b], apex, sph[k, :3], r[k] + 2 * pad + wid):
+                    L.append(k)
+                    if len(L) > 7:
+                        break
+            lists[(key, b)] = L if len(L) <= 7 else None
+        return lists[(key, b)]
+    dl_res = dl_tests = 0
+
     rng = np.random.default_rng(5)
     parked = caught = parked_ground = parked_bvh = gcaught = 0
     traced = 0
@@ -160,6 +180,14 @@ def main():
                 continue
             parked += 1
             if big[h]:
+                cell = tuple(int(math.floor(o[q] / g)) for q in range(3))
+                L = dlist(('c',) + cell, cube_bin(d, N), (np.array(cell, dtype=float) + 0.5) * g, 0.8661 * g)
+            else:
+                L = dlist(int(h), cube_bin(d, N), sph[h, :3], r[h] + pad)
+            if L is not None:
+                dl_res += 1
+                dl_tests += len(L)
+            if big[h]:
                 parked_ground += 1
                 if h == gq and gempty(o, cube_bin(d, N)):
                     gcaught += 1
@@ -172,7 +200,9 @@ def main():
           f"N={N} ({nbins} bins): caught {caught} = {caught / max(1, parked):.3f} of parked, "
           f"{caught / max(1, parked_bvh):.3f} of BVH-origin parked; table entries built {len(table)}; "
           f"ground column table: caught {gcaught} = {gcaught / max(1, parked_ground):.3f} of "
-          f"ground-origin parked; total {(caught + gcaught) / max(1, parked):.3f} of parked")
+          f"ground-origin parked; total {(caught + gcaught) / max(1, parked):.3f} of parked; "
+          f"direction lists (<= 7) resolve {dl_res / max(1, parked):.3f} of parked, "
+          f"mean list {dl_tests / max(1, dl_res):.2f}")
 
 
 if __name__ == "__main__":

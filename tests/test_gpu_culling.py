@@ -351,13 +351,14 @@ def test_far_camera_rebase_bit_exact(oracle_mod, final_scene):
 
 
 def test_enclosing_sky_sphere(oracle_mod, final_scene):
-    """a non-BVH sphere of radius 1e12 around the final scene. Every
-    ray that leaves the scene hits it from inside and scatters back from ~1e12
-    out, beyond 8 r_check: those rays take the reference's scan
-    while the scene's rays keep the culled paths. Frame and ray count equal the
-    oracle's, and probe rays from the sky sphere's surface into the scene
-    equal the linear sweep."""
-    sph = np.concatenate([final_scene, [[0.0, 0.0, 0.0, 1e12]]])
+    """a non-BVH sphere around the final scene, of radius 1e6 (the
+    largest coordinate the culling structure accepts; beyond it the whole scene
+    takes the linear scan). Every ray that leaves the scene hits it from inside
+    and scatters back from ~1e6 out, beyond 8 r_check: those rays take the
+    reference's scan while the scene's rays keep the culled
+    paths. Frame and ray count equal the oracle's, and probe rays from the sky
+    sphere's surface into the scene equal the linear sweep."""
+    sph = np.concatenate([final_scene, [[0.0, 0.0, 0.0, 1e6]]])
     cam = P.camera_look_at(aspect=48 / 32)
     a, _, sa = P.render(sph, cam, 48, 32, 2, seed=7, cull_stats=True)
     want, _, rays = oracle_mod.render(sph, cam, 48, 32, 2, seed=7, threads=8)
@@ -366,7 +367,7 @@ def test_enclosing_sky_sphere(oracle_mod, final_scene):
     rng = np.random.default_rng(43)
     n = 50_000
     u = rng.normal(size=(n, 3))
-    o = 1e12 * u / np.linalg.norm(u, axis=1, keepdims=True)
+    o = 1e6 * u / np.linalg.norm(u, axis=1, keepdims=True)
     d = final_scene[rng.integers(1, len(final_scene), n), :3] + rng.normal(scale=0.3, size=(n, 3)) - o
     _compare(sph, o, d)
 
