@@ -103,8 +103,6 @@ struct Tuning {
   double stamps = 0;         // diagnostic kernel variant (section clocks, utilisation probes)
   double scene_rebuild = 0;  // rebuild the culling structures for an unchanged scene
   double big_ratio = 0;      // radius ratio of the big-sphere class (0: psrt_bvh's default)
-  double no_dirlist = 0;     // material kernel without its direction lists (every unbounded ray walks)
-  double dl_cells = 1;       // direction lists keyed by lattice cells for big-sphere origins (0: none)
 };
 }  // namespace psrt
 
@@ -122,8 +120,7 @@ const TuningKey kTuningKeys[] = {
     {"blocks_per_cu", &psrt::Tuning::blocks_per_cu}, {"mat_lds", &psrt::Tuning::mat_lds},
     {"mat_batch", &psrt::Tuning::mat_batch},         {"flush_at", &psrt::Tuning::flush_at},
     {"stamps", &psrt::Tuning::stamps},               {"scene_rebuild", &psrt::Tuning::scene_rebuild},
-    {"big_ratio", &psrt::Tuning::big_ratio},         {"no_dirlist", &psrt::Tuning::no_dirlist},
-    {"dl_cells", &psrt::Tuning::dl_cells},
+    {"big_ratio", &psrt::Tuning::big_ratio},
 };
 std::mutex g_tuning_mu;
 psrt::Tuning g_tuning;  // the process defaults (rt_context_set_tuning(NULL, ...))
@@ -221,13 +218,6 @@ struct rt_context {
   rt_camera_lens lcam{};
   int* d_path = nullptr;  // per resident lane, its path's attenuating hits
   size_t path_cap = 0;    // ints
-  // the material kernel's direction lists (MatArgs::dl), built with the
-  // materials (build_dir_lists) for the current scene; nullptr: none
-  uint4* d_dl = nullptr;
-  int* d_dl_slot = nullptr;
-  double dl_lo[3] = {0, 0, 0}, dl_inv = 0.0;
-  int dl_dims[3] = {0, 0, 0};
-  std::vector<int> big_host;  // the scene's big-sphere indices (BvhHost::big_idx)
   rt_stats last{};
   int n_last = 0;
   bool last_mat = false;  // the last render used RT_FLAG_MATERIALS (no stamps to read)
@@ -407,8 +397,6 @@ int rt_context_destroy(rt_context* c) {
   (void)hipFree(c->d_nb_rec);
   (void)hipFree(c->d_mats);
   (void)hipFree(c->d_path);
-  (void)hipFree(c->d_dl);
-  (void)hipFree(c->d_dl_slot);
   for (auto e : c->ev) (void)hipEventDestroy(e);
   if (c->ev_all0) (void)hipEventDestroy(c->ev_all0);
   if (c->ev_all1) (void)hipEventDestroy(c->ev_all1);
@@ -456,10 +444,6 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
   c->scene.clear();  // set again once every structure is built
   c->has_mats = false;  // materials belong to the scene they were set for
   c->mat_plist_valid = false;
-  (void)hipFree(c->d_dl);  // so do the direction lists (built with the materials)
-  (void)hipFree(c->d_dl_slot);
-  c->d_dl = nullptr, c->d_dl_slot = nullptr;
-  c->big_host.clear();
   const int cap = n > 0 ? n : 1;
   if (cap > c->n_cap) {
     (void)hipFree(c->d_geo);
@@ -543,7 +527,6 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
       HIP_TRY(up(c->d_big, b.big_idx.data(), b.big_idx.size() * sizeof(int)));
     c->pgrid = b.grid;
     c->pad = b.pad;
-    c->big_host = b.big_idx;
     const size_t ns = b.grid.start.size(), ni = std::max<size_t>(1, b.grid.items.size());
     HIP_TRY(hipMalloc(&c->d_cell_start, ns * sizeof(int)));
     HIP_TRY(hipMalloc(&c->d_cell_items, ni * sizeof(int)));
@@ -883,11 +866,6 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     ma.path = c->d_path;
     ma.path_stride = (unsigned)lanes;
     ma.batch = (unsigned)std::max(1.0, c->tune.mat_batch);
-    ma.dl = c->tune.no_dirlist ? nullptr : c->d_dl;
-    ma.dl_slot = c->d_dl_slot;
-    for (int k = 0; k < 3; ++k) ma.dl_lo[k] = c->dl_lo[k], ma.dl_dims[k] = c->dl_dims[k];
-    ma.dl_inv = c->dl_inv;
-    ma.dl_pad = c->pad;
   }
 
   psrt::TraceArgs ta{};
@@ -1395,96 +1373,6 @@ int rt_render(const rt_sphere* sph, int n, const rt_camera* cam, const rt_params
   return RT_OK;
 }
 
-// The material kernel's direction lists (MatArgs::dl, psrt_mat_dir_lists;
-// DESIGN.md §14) for the current scene: rows [0, n) keyed by the BVH sphere a
-// bounce ray starts on, rows [n, n + slots) by the cell of a lattice (the point
-// grid's cell edge, over the BVH spheres' padded bounds widened by one cell)
-// that a big sphere's surface crosses. Built on the device, on the context's
-// stream; none without a BVH, or (cells only) when the lattice would pass
-// kDirCellCap cells.
-static int build_dir_lists(rt_context* c) {
-  (void)hipFree(c->d_dl);
-  (void)hipFree(c->d_dl_slot);
-  c->d_dl = nullptr, c->d_dl_slot = nullptr;
-  if (!c->bvh || c->n_leaf == 0 || c->n >= (int)psrt::kCamOverflow) return RT_OK;
-  constexpr long kDirCellCap = 1L << 22;
-  const double edge = 1.0 / (double)c->pgrid.finv;
-  std::vector<char> is_big((size_t)c->n, 0);
-  for (int b : c->big_host) is_big[(size_t)b] = 1;
-  double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
-  for (int k = 0; k < c->n; ++k) {
-    if (is_big[(size_t)k]) continue;
-    const rt_sphere& q = c->scene.empty() ? rt_sphere{} : c->scene[(size_t)k];
-    const double ctr[3] = {q.cx, q.cy, q.cz}, r = std::fabs(q.r) + c->pad;
-    for (int a = 0; a < 3; ++a) lo[a] = std::min(lo[a], ctr[a] - r), hi[a] = std::max(hi[a], ctr[a] + r);
-  }
-  int dims[3] = {0, 0, 0};
-  long ncell = 1;
-  const bool fin = std::isfinite(edge) && edge > 0.0;
-  for (int a = 0; a < 3 && fin; ++a) {
-    lo[a] -= edge, hi[a] += edge;
-    const double d = std::ceil((hi[a] - lo[a]) / edge);
-    dims[a] = d >= 1.0 && d < 1e6 ? (int)d : 0;
-    ncell *= dims[a];
-  }
-  std::vector<int> slot_of, slot_cell;
-  if (fin && ncell > 0 && ncell <= kDirCellCap && !c->big_host.empty() && c->tune.dl_cells != 0) {
-    // a slot for each cell some big sphere's surface passes within half a
-    // diagonal (+ pad) of the cell's centre
-    slot_of.assign((size_t)ncell, -1);
-    const double hd = 0.8660254037844387 * edge * (1.0 + 0x1p-20) + c->pad;
-    for (int x = 0; x < dims[0]; ++x)
-      for (int y = 0; y < dims[1]; ++y)
-        for (int z = 0; z < dims[2]; ++z) {
-          const double cc[3] = {lo[0] + (x + 0.5) * edge, lo[1] + (y + 0.5) * edge,
-                                lo[2] + (z + 0.5) * edge};
-          bool on = false;
-          for (int b : c->big_host) {
-            const rt_sphere& q = c->scene[(size_t)b];
-            const double dx = cc[0] - q.cx, dy = cc[1] - q.cy, dz = cc[2] - q.cz;
-            const double l = std::sqrt(dx * dx + dy * dy + dz * dz);
-            on = on || std::fabs(l - std::fabs(q.r)) <= hd;
-          }
-          if (on) {
-            const long cell = ((long)x * dims[1] + y) * dims[2] + z;
-            slot_of[(size_t)cell] = (int)slot_cell.size();
-            slot_cell.push_back((int)cell);
-          }
-        }
-  }
-  const size_t rows = (size_t)c->n + slot_cell.size();
-  HIP_TRY(hipMalloc(&c->d_dl, rows * psrt::kDirBins * sizeof(uint4)));
-  HIP_TRY(hipMalloc(&c->d_dl_slot, std::max<size_t>(1, slot_of.size()) * sizeof(int)));
-  int* d_slot_cell = nullptr;
-  HIP_TRY(hipMalloc(&d_slot_cell, std::max<size_t>(1, slot_cell.size()) * sizeof(int)));
-  if (!slot_of.empty())
-    HIP_TRY(hipMemcpyAsync(c->d_dl_slot, slot_of.data(), slot_of.size() * sizeof(int),
-                           hipMemcpyHostToDevice, c->stream));
-  if (!slot_cell.empty())
-    HIP_TRY(hipMemcpyAsync(d_slot_cell, slot_cell.data(), slot_cell.size() * sizeof(int),
-                           hipMemcpyHostToDevice, c->stream));
-  psrt::MatDirArgs da{};
-  da.geo = c->d_geo;
-  da.n = c->n;
-  da.leaf_geo = c->d_leaf_geo;
-  da.leaf_idx = c->d_leaf_idx;
-  da.n_leaf = c->n_leaf;
-  da.big_idx = c->d_big;
-  da.n_big = c->n_big;
-  da.slot_cell = d_slot_cell;
-  for (int a = 0; a < 3; ++a) da.lo[a] = lo[a], da.dims[a] = std::max(1, dims[a]);
-  da.edge = edge;
-  da.pad = c->pad;
-  da.dl = c->d_dl;
-  hipLaunchKernelGGL(psrt::psrt_mat_dir_lists, dim3((unsigned)rows, 6), dim3(64), 0, c->stream, da);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  (void)hipFree(d_slot_cell);
-  for (int a = 0; a < 3; ++a) c->dl_lo[a] = lo[a], c->dl_dims[a] = slot_of.empty() ? 0 : dims[a];
-  c->dl_inv = 1.0 / edge;
-  return RT_OK;
-}
-
 int rt_context_set_materials(rt_context* c, const rt_material* mats, int n,
                              const rt_camera_lens* cam) {
   if (!c) return set_error(RT_E_INVALID, "rt_context_set_materials: ctx is NULL");
@@ -1527,10 +1415,6 @@ int rt_context_set_materials(rt_context* c, const rt_material* mats, int n,
   }
   c->lcam = *cam;
   c->mat_plist_valid = false;
-  {
-    const int rc = build_dir_lists(c);
-    if (rc) return rc;
-  }
   c->has_mats = true;
   return RT_OK;
 }

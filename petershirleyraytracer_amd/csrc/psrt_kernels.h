@@ -255,35 +255,6 @@ struct MatArgs {
   // per-pixel candidate lists of the camera rays through the lens
   // (psrt_mat_camera_lists; CamListArgs format), or nullptr
   const uint4* __restrict__ plist;
-  // direction lists (psrt_mat_dir_lists), or nullptr: per
-  // origin key and cube-map direction bin, every BVH sphere a bounce ray from
-  // that key's region in that bin can meet, in the plist record format. Keys
-  // [0, n): BVH sphere j (the ray starts on j's surface); [n, n + slots): the
-  // cells of a lattice over the BVH spheres' bounds that a big sphere's
-  // surface crosses (dl_slot: cell -> slot, -1 none)
-  const uint4* __restrict__ dl;        // [(n + slots) * kDirBins]
-  const int* __restrict__ dl_slot;     // [dl_dims[0] * dl_dims[1] * dl_dims[2]]
-  double dl_lo[3], dl_inv, dl_pad;     // lattice origin, 1 / cell edge; the BVH pad
-  int dl_dims[3];
-};
-
-// Direction lists: kDirN x kDirN bins per cube-map face (face 2 axis + (d_axis
-// < 0); bin (i, j) over the other two coordinates in axis order, each divided
-// by |d_axis|)
-constexpr int kDirN = 8;
-constexpr int kDirBins = 6 * kDirN * kDirN;
-struct MatDirArgs {
-  const double4* __restrict__ geo;       // spheres {c, r*r} by index
-  int n;
-  const double4* __restrict__ leaf_geo;  // BVH spheres per leaf slot
-  const int* __restrict__ leaf_idx;
-  int n_leaf;
-  const int* __restrict__ big_idx;
-  int n_big;
-  const int* __restrict__ slot_cell;     // [slots]: the lattice cell of each slot
-  double lo[3], edge, pad;
-  int dims[3];
-  uint4* __restrict__ dl;                // [(n + slots) * kDirBins]
 };
 
 // Camera-ray candidate lists for the thin lens (psrt_mat_camera_lists):
@@ -329,7 +300,6 @@ __global__ void psrt_trace_mat(const double4* __restrict__ geo, const double* __
 // psrt_reduce over colour records: samp_t holds [pixels][s_count][3] doubles
 __global__ void psrt_reduce_rgb(ReduceArgs a);
 __global__ void psrt_mat_camera_lists(MatCamListArgs a);
-__global__ void psrt_mat_dir_lists(MatDirArgs a);
 
 template <bool kBVH, bool kStamps, bool kLds, bool kCount>
 __global__ void psrt_trace(const double4* __restrict__ geo, const double* __restrict__ inv_r,

@@ -104,67 +104,6 @@ __device__ __forceinline__ void test_sphere_m(const double4 s, int idx, double o
   }
 }
 
-// Cube-map bin of a direction (MatArgs::dl, psrt_mat_dir_lists), in FP32:
-// face = the axis of the largest |d_k| (ties to the lower axis) and its sign;
-// (i, j) over the other two coordinates in axis order, each divided by that
-// one, kDirN per face edge. The FP32 rounding moves a direction by ~2^-22 rad,
-// far inside the 1e-6 rad the lists' cones are widened by.
-__device__ __forceinline__ int dir_bin(double dx, double dy, double dz) {
-  const float x = (float)dx, y = (float)dy, z = (float)dz;
-  const float ax = __builtin_fabsf(x), ay = __builtin_fabsf(y), az = __builtin_fabsf(z);
-  const bool fx = ax >= ay && ax >= az;
-  const bool fy = !fx && ay >= az;
-  const float m = fx ? ax : (fy ? ay : az);
-  const float u = fx ? y : x;  // face x: (y, z); y: (x, z); z: (x, y)
-  const float v = fx ? z : (fy ? z : y);
-  const float w = fx ? x : (fy ? y : z);
-  const float h = 0.5f * kDirN;
-  const float k = h / m;
-  const int i = min(kDirN - 1, max(0, (int)__builtin_floorf(__builtin_fmaf(u, k, h))));
-  const int j = min(kDirN - 1, max(0, (int)__builtin_floorf(__builtin_fmaf(v, k, h))));
-  const int face = 2 * (fx ? 0 : (fy ? 1 : 2)) + (w < 0.0f ? 1 : 0);
-  return (face * kDirN + j) * kDirN + i;
-}
-
-// The direction list of a bounce ray from sphere `from` (the hit it leaves),
-// or an overflow record when none applies (psrt_mat_dir_lists). From a BVH
-// sphere j the key is j itself, once o is checked to lie within |r_j| + pad of
-// c_j (a hit point on j does: the BVH pad bounds the root error); from a big
-// sphere, the lattice cell holding o, if that cell has a slot. Read at the
-// scatter, a loop iteration before hit_quick_m needs it, so the table's
-// latency (an L2 / Infinity Cache read) overlaps the rest of the iteration.
-__device__ __forceinline__ uint4 dir_list_of(const MatArgs& a, const BvhView& bv,
-                                             const int* __restrict__ big_idx,
-                                             const double4* __restrict__ geo, int n, int from,
-                                             double ox, double oy, double oz, double dx, double dy,
-                                             double dz, double A) {
-  uint4 rec = make_uint4(kCamOverflow, 0u, 0u, 0u);
-  const double am = __builtin_fmax(__builtin_fabs(ox),
-                                   __builtin_fmax(__builtin_fabs(oy), __builtin_fabs(oz)));
-  // (A in range: dir_bin's FP32 direction is finite and normal)
-  if (!(am <= bv.r_check && A >= 0x1p-100 && A <= 0x1p100)) return rec;
-  bool big = false;
-  for (int b = 0; b < bv.n_big; ++b) big |= big_idx[b] == from;
-  int row = -1;
-  if (!big) {
-    const double4 s = geo[from];
-    const double ax = ox - s.x, ay = oy - s.y, az = oz - s.z;
-    const double R = __builtin_sqrt(s.w) + a.dl_pad;
-    if ((ax * ax + ay * ay) + az * az <= R * R) row = from;
-  } else {
-    const double fx = (ox - a.dl_lo[0]) * a.dl_inv, fy = (oy - a.dl_lo[1]) * a.dl_inv,
-                 fz = (oz - a.dl_lo[2]) * a.dl_inv;
-    if (fx >= 0.0 && fy >= 0.0 && fz >= 0.0 && fx < (double)a.dl_dims[0] &&
-        fy < (double)a.dl_dims[1] && fz < (double)a.dl_dims[2]) {
-      const int cell = ((int)fx * a.dl_dims[1] + (int)fy) * a.dl_dims[2] + (int)fz;
-      const int slot = a.dl_slot[cell];
-      if (slot >= 0) row = n + slot;
-    }
-  }
-  if (row >= 0) rec = a.dl[(size_t)row * kDirBins + dir_bin(dx, dy, dz)];
-  return rec;
-}
-
 // hittable_list::hit(r, 0.001, inf) for one lane, cheap part: the big
 // spheres, then the point-location grid for the segment [o, o + bt d] (as
 // psrt_trace's hit_quick: a sphere with an accepted root t <= bt has its hit
@@ -176,8 +115,7 @@ __device__ __forceinline__ bool hit_quick_m(TestCount<kCount>& nt, TestCount<kCo
                                             const double4* __restrict__ geo,
                                             int n, const BvhView& bv,
                                             const int* __restrict__ big_idx, const GridC& gc,
-                                            uint4 rec, const uint4 dlrec,
-                                            double ox, double oy, double oz, double dx,
+                                            uint4 rec, double ox, double oy, double oz, double dx,
                                             double dy, double dz, double A, double& bt, int& bi) {
   bt = __builtin_inf();
   bi = -1;
@@ -196,12 +134,8 @@ __device__ __forceinline__ bool hit_quick_m(TestCount<kCount>& nt, TestCount<kCo
     test_sphere_m(geo[idx], idx, ox, oy, oz, dx, dy, dz, A, bt, bi);
   }
   nt.add((unsigned)bv.n_big);
-  // a bounce ray nothing has bounded yet: its direction list (dir_list_of,
-  // read at the scatter before this bounce), when one applies
-  if (bt == __builtin_inf() && (dlrec.x & 0xFFFFu) != kCamOverflow) rec = dlrec;
-  // a camera ray with its pixel's candidate list (psrt_mat_camera_lists), or a
-  // bounce ray with its direction list: the listed BVH spheres are every one
-  // the ray can hit
+  // a camera ray with its pixel's candidate list (psrt_mat_camera_lists): the
+  // listed BVH spheres are every one a ray of the pixel can hit
   const unsigned ncand = rec.x & 0xFFFFu;
   if (ncand != kCamOverflow) {
     uint64_t lo = rec.x | (uint64_t)rec.y << 32, hi = rec.z | (uint64_t)rec.w << 32;
@@ -422,7 +356,6 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
   bool pending = false;
   int pbi = -1;
   double pbt = 0.0;
-  uint4 dlrec = make_uint4(kCamOverflow, 0u, 0u, 0u);  // the next bounce's direction list
   // RT_FLAG_CULL_STATS: executed FP64 sphere tests (every test here is a full
   // one: no pre-reject), FP32 box tests, FP64 root-box tests
   TestCount<kCount> ntests, nboxes, nroots;
@@ -491,9 +424,8 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
         __builtin_amdgcn_s_setprio(kMatHitPrio);
         uint4 rec = make_uint4(kCamOverflow, 0u, 0u, 0u);
         if (k == 0 && a.plist) rec = a.plist[pq];  // camera ray: its pixel's list
-        decided = hit_quick_m<kBVH>(ntests, nroots, lgeo, a.n, bv, big_idx, gc, rec,
-                                    k > 0 ? dlrec : make_uint4(kCamOverflow, 0u, 0u, 0u),
-                                    ox, oy, oz, dx, dy, dz, A, pbt, pbi);
+        decided = hit_quick_m<kBVH>(ntests, nroots, lgeo, a.n, bv, big_idx, gc, rec, ox, oy, oz,
+                                    dx, dy, dz, A, pbt, pbi);
         PSRT_MAT_ABLATE_AT(HIT);
         __builtin_amdgcn_s_setprio(0);
         pending = !decided;
@@ -617,9 +549,6 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
         dx = ndx, dy = ndy, dz = ndz;
         A = (dx * dx + dy * dy) + dz * dz;
         ++k;
-        if constexpr (kBVH) {
-          if (a.dl) dlrec = dir_list_of(a, bv, big_idx, lgeo, a.n, bi, ox, oy, oz, dx, dy, dz, A);
-        }
       }
     }
     if (fin) {
@@ -826,107 +755,6 @@ __global__ __launch_bounds__(64) void psrt_mat_camera_lists(MatCamListArgs a) {
     if (!full) w[0] = (w[0] & 0xFFFF0000u) | n;
   }
   a.plist[(size_t)rk * a.width + px] = make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-// ---- direction lists (MatArgs::dl) ---------------------------
-//
-// A bounce ray starts at o, the previous hit. Key j (a BVH sphere): o lies
-// within w = |r_j| + pad of c_j; key = a lattice cell: o lies within w = half
-// the cell's diagonal of its centre (both widened below). Its direction d is
-// in bin b, i.e. inside the bin's cone C_b (apex 0; half-angle to the bin's
-// corners + 1e-6 rad). A point q = o + t d of the ray then lies within w of
-// the cone apex + C_b (apex = c_j or the cell centre): q - (o - apex) is on
-// it. A sphere k with an accepted root has its hit point within pad of its
-// surface (the BVH's root-error pad), so the cone meets the ball (c_k, |r_k| +
-// pad + w): the list holds every such k (and j itself, which a ray leaving j
-// inward can re-hit), in leaf order, or overflows past kCamPixelCap. The FP64
-// cone test is widened (radius x (1 + 2^-20), angle 1e-6 rad), margins far
-// above its rounding and the device's FP32 bin choice (~2^-22 rad).
-//
-// One wave per (key, face): lane = the bin (i, j) within the face.
-#ifndef PSRT_DIR_CAP
-#define PSRT_DIR_CAP 7  // entries of a direction list (<= kCamPixelCap); longer: the walk
-#endif
-__global__ __launch_bounds__(64) void psrt_mat_dir_lists(MatDirArgs a) {
-  static_assert(kDirN * kDirN == 64, "one wave per face");
-  const int row = blockIdx.x, face = blockIdx.y, lane = (int)threadIdx.x;
-  const int ci = lane % kDirN, cj = lane / kDirN;
-  const int f = face >> 1, uo = f == 0 ? 1 : 0, vo = f == 2 ? 1 : 2;
-  const double sg = (face & 1) ? -1.0 : 1.0;
-  double apex[3], wid;
-  int self = -1;
-  bool ok = true;
-  if (row < a.n) {
-    for (int b = 0; b < a.n_big; ++b) ok = ok && a.big_idx[b] != row;
-    const double4 g = a.geo[row];
-    apex[0] = g.x, apex[1] = g.y, apex[2] = g.z;
-    wid = __builtin_sqrt(g.w) + a.pad;
-    self = row;
-  } else {
-    const int cell = a.slot_cell[row - a.n];
-    const int cz = cell % a.dims[2], cy = (cell / a.dims[2]) % a.dims[1],
-              cx = cell / (a.dims[2] * a.dims[1]);
-    apex[0] = a.lo[0] + (cx + 0.5) * a.edge;
-    apex[1] = a.lo[1] + (cy + 0.5) * a.edge;
-    apex[2] = a.lo[2] + (cz + 0.5) * a.edge;
-    wid = 0.8660254037844387 * a.edge + 0x1p-20 * a.edge;  // sqrt(3)/2: half the diagonal
-  }
-  // the bin's cone: axis through the bin's centre on the face, half-angle to
-  // its farthest corner (the bin is a planar quadrilateral on the face)
-  auto dir = [&](double s, double t, double d[3]) {
-    d[f] = sg, d[uo] = s, d[vo] = t;
-    const double il = 1.0 / __builtin_sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
-    d[0] *= il, d[1] *= il, d[2] *= il;
-  };
-  const double step = 2.0 / kDirN;
-  const double s0 = -1.0 + ci * step, t0 = -1.0 + cj * step;
-  double ax[3], d[3];
-  dir(s0 + 0.5 * step, t0 + 0.5 * step, ax);
-  double cmin = 1.0;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    dir((e & 1) ? s0 + step : s0, (e >> 1) ? t0 + step : t0, d);
-    cmin = __builtin_fmin(cmin, (ax[0] * d[0] + ax[1] * d[1]) + ax[2] * d[2]);
-  }
-  const double ca = cmin - 1e-6;  // cos(alpha + delta) >= cos(alpha) - delta
-  const double sa = __builtin_sqrt(__builtin_fmax(0.0, 1.0 - ca * ca));
-  unsigned w[4] = {0u, 0u, 0u, 0u};
-  unsigned cnt = 0;
-  bool full = !ok;
-  if (ok && self >= 0) {
-    ++cnt;
-    w[0] |= (unsigned)self << 16;  // slot 1: j itself
-  }
-  for (int e = 0; e < a.n_leaf && !full; ++e) {
-    const int k = a.leaf_idx[e];
-    if (k == self) continue;
-    const double4 q = a.leaf_geo[e];
-    const double cx = q.x - apex[0], cy = q.y - apex[1], cz = q.z - apex[2];
-    const double l2 = (cx * cx + cy * cy) + cz * cz;
-    const double R = (__builtin_sqrt(q.w) + a.pad + wid) * (1.0 + 0x1p-20);
-    bool meets = !(l2 > R * R);  // apex inside / near the ball (or NaN)
-    if (!meets) {
-      const double l = __builtin_sqrt(l2);
-      const double cb = ((ax[0] * cx + ax[1] * cy) + ax[2] * cz) / l;
-      if (cb >= ca) {
-        meets = true;  // centre inside the cone
-      } else {
-        const double sb = __builtin_sqrt(__builtin_fmax(0.0, 1.0 - cb * cb));
-        const double cosd = cb * ca + sb * sa, sind = sb * ca - cb * sa;
-        meets = cosd >= 0.0 && sind <= R / l;
-      }
-    }
-    if (!meets) continue;
-    if (cnt == (unsigned)PSRT_DIR_CAP) {
-      full = true;
-      break;
-    }
-    ++cnt;  // slot cnt of 8 uint16 (slot 0 = count)
-    w[cnt >> 1] |= (unsigned)k << ((cnt & 1) * 16);
-  }
-  w[0] = (w[0] & 0xFFFF0000u) | (full ? kCamOverflow : cnt);
-  const int bin = (face * kDirN + cj) * kDirN + ci;
-  a.dl[(size_t)row * kDirBins + bin] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 }  // namespace psrt

@@ -239,39 +239,14 @@ def _contact_mat_scene(rng):
     return np.array(sp), np.array(mt, dtype=float)
 
 
-def test_direction_lists_are_bit_identical(oracle_mod, book, knobs):
-    """Bounce rays the big spheres leave unbounded test their direction list
-    (psrt_mat_dir_lists) instead of walking the BVH: frames equal
-    the ones without lists (tuning knob no_dirlist) and the oracle's, on the
-    book scene and on contact scenes with two big surfaces, and the lists
-    remove most of the walk's box tests."""
-    from petershirleyraytracer_amd.render import FLAG_CULL_STATS
-    sp, mt, _ = book
-    cases = [(sp, mt, oracle_mod.camera_look_at_lens(aspect=1.5), 120, 80, 6)]
+def test_contact_scenes_two_big_surfaces(oracle_mod):
+    """Touching, nested and hollow spheres between a ground and a second big
+    sphere standing as a wall (the scenes the r05 direction-list experiment
+    was checked on, profiles/r05_dirlist): frames equal the oracle's."""
     for seed in (1, 2):
-        csp, cmt = _contact_mat_scene(np.random.default_rng(seed))
-        cases.append((csp, cmt, oracle_mod.camera_look_at_lens((3.0, 2.0, 6.0), (0.0, 0.3, 0.0),
-                                                               (0, 1, 0), 50.0, 1.5, 0.05, 6.0),
-                      90, 60, 4))
-    for i, (s, m, lens, W, H, spp) in enumerate(cases):
-        acc, _, st = P.render_materials(s, m, _lens(lens), W, H, spp, 50, 7)
-        knobs("no_dirlist", 1)
-        acc2, _, st2 = P.render_materials(s, m, _lens(lens), W, H, spp, 50, 7)
-        knobs("no_dirlist", 0)
-        assert np.array_equal(bits(acc), bits(acc2)) and st["rays"] == st2["rays"], i
-        ref, rays = oracle_mod.render_mat(s, m, lens, W, H, spp, 50, 7, threads=8)
-        assert np.array_equal(bits(acc), bits(ref)) and st["rays"] == rays, i
-    # the counting variant on the book scene: fewer slab tests with the lists
-    boxes = []
-    for off in (0, 1):
-        knobs("no_dirlist", off)
-        ctx = P.Context(0)
-        try:
-            lens = cases[0][2]
-            ctx.set_scene(sp, lens["base"])
-            ctx.set_materials(mt, _lens(lens))
-            ctx.render_device(P.params(120, 80, 6, 50, 7, flags=FLAG_MATERIALS | FLAG_CULL_STATS))
-            boxes.append(ctx.sync_stats()["box_tests"])
-        finally:
-            ctx.close()
-    assert boxes[0] < 0.6 * boxes[1], boxes
+        s, m = _contact_mat_scene(np.random.default_rng(seed))
+        lens = oracle_mod.camera_look_at_lens((3.0, 2.0, 6.0), (0.0, 0.3, 0.0), (0, 1, 0), 50.0,
+                                              1.5, 0.05, 6.0)
+        acc, _, st = P.render_materials(s, m, _lens(lens), 90, 60, 4, 50, 7)
+        ref, rays = oracle_mod.render_mat(s, m, lens, 90, 60, 4, 50, 7, threads=8)
+        assert np.array_equal(bits(acc), bits(ref)) and st["rays"] == rays, seed
