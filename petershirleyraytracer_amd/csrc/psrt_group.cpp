@@ -76,18 +76,24 @@ int member_render(Member& mb, int g, int G, const rt_params& p, double* accum,
   int rc = rt_render_device(mb.ctx, &q, mb.d_accum, rgb8 ? mb.d_rgb : nullptr, nullptr);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)rt_context_stream(mb.ctx);
+  // Once a copy into the caller's buffers is enqueued, every return waits for
+  // the stream: no copy may still write them after rt_group_render returns.
+  auto fail = [&](int code) {
+    (void)hipStreamSynchronize(s);
+    return code;
+  };
   // row k of this member is row g + kG of the caller's shard
   const size_t W3 = (size_t)q.width * 3;
   if (accum &&
       (e = hipMemcpy2DAsync(accum + (size_t)g * W3, (size_t)G * W3 * sizeof(double), mb.d_accum,
                             W3 * sizeof(double), W3 * sizeof(double), (size_t)rows,
                             hipMemcpyDeviceToHost, s)) != hipSuccess)
-    return hip_err(e, "hipMemcpy2DAsync");
+    return fail(hip_err(e, "hipMemcpy2DAsync"));
   if (rgb8 && (e = hipMemcpy2DAsync(rgb8 + (size_t)g * W3, (size_t)G * W3, mb.d_rgb, W3, W3,
                                     (size_t)rows, hipMemcpyDeviceToHost, s)) != hipSuccess)
-    return hip_err(e, "hipMemcpy2DAsync");
+    return fail(hip_err(e, "hipMemcpy2DAsync"));
   rc = rt_context_sync_stats(mb.ctx, st);  // waits for the render
-  if (rc) return rc;
+  if (rc) return fail(rc);
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_err(e, "hipStreamSynchronize");
   return RT_OK;
 }

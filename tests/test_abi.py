@@ -113,6 +113,25 @@ def test_bad_arguments_are_errors():
     assert L.rt_render(None, 0, None, C.byref(p), acc, None, None) == -1
 
 
+def test_group_bad_arguments_are_errors():
+    """rt_group_* argument checks need no device; without one, creating a
+    group fails with the context's error and leaves no group behind."""
+    L = _lib.load()
+    out = C.c_void_p()
+    devs = (C.c_int * 2)(0, 0)
+    assert L.rt_group_create(None, 2, C.byref(out)) == -1
+    assert L.rt_group_create(devs, 0, C.byref(out)) == -1
+    assert L.rt_group_create(devs, 2, None) == -1
+    assert L.rt_group_size(None) == 0 and not L.rt_group_context(None, 0)
+    assert L.rt_group_destroy(None) == 0
+    p = P.params(4, 4, 1)
+    assert L.rt_group_render(None, C.byref(p), None, None, None) == -1
+    assert L.rt_group_set_scene(None, None, 0, None) == -1
+    if not have_gpu():
+        rc = L.rt_group_create(devs, 2, C.byref(out))
+        assert rc in (-2, -3) and not out.value, rc
+
+
 @pytest.mark.skipif(have_gpu(), reason="checks the no-device path")
 def test_render_without_device_fails_loudly():
     with pytest.raises(_lib.RtError) as e:
