@@ -60,22 +60,32 @@ int usage() {
 }
 
 // --devices: "N" = devices 0..N-1; "a,b,c" = those members (repeats allowed)
+// a non-negative decimal integer, the whole string
+bool parse_index(const std::string& s, int& out) {
+  if (s.empty() || s.size() > 6 || s.find_first_not_of("0123456789") != std::string::npos)
+    return false;
+  out = std::atoi(s.c_str());
+  return true;
+}
+
+// --devices N (devices 0..N-1) | D0,D1,... (a member per entry; repeats allowed)
 bool parse_devices(const std::string& v, std::vector<int>& out) {
   out.clear();
   if (v.find(',') == std::string::npos) {
-    const int n = std::atoi(v.c_str());
-    if (n < 1) return false;
+    int n = 0;
+    if (!parse_index(v, n) || n < 1 || n > 1024) return false;
     for (int d = 0; d < n; ++d) out.push_back(d);
     return true;
   }
   size_t a = 0;
   while (a <= v.size()) {
     const size_t b = std::min(v.find(',', a), v.size());
-    if (b == a) return false;
-    out.push_back(std::atoi(v.substr(a, b - a).c_str()));
+    int d = 0;
+    if (!parse_index(v.substr(a, b - a), d)) return false;
+    out.push_back(d);
     a = b + 1;
   }
-  return !out.empty();
+  return !out.empty() && out.size() <= 1024;
 }
 
 }  // namespace
