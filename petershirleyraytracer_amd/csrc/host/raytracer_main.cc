@@ -17,6 +17,7 @@
 //                                   # the book's materials + thin lens
 #include <chrono>
 #include <cstdio>
+#include <climits>
 #include <cstdlib>
 #include <fstream>
 #include <iostream>
@@ -60,6 +61,26 @@ int usage() {
 }
 
 // --devices: "N" = devices 0..N-1; "a,b,c" = those members (repeats allowed)
+// a decimal integer / a floating-point number, the whole string
+bool parse_int(const char* s, int& out) {
+  char* end = nullptr;
+  const long v = std::strtol(s, &end, 10);
+  if (end == s || *end != '\0' || v < INT_MIN || v > INT_MAX) return false;
+  out = (int)v;
+  return true;
+}
+bool parse_u64(const char* s, unsigned long long& out) {
+  char* end = nullptr;
+  if (*s == '-') return false;
+  out = std::strtoull(s, &end, 10);
+  return end != s && *end == '\0';
+}
+bool parse_double(const char* s, double& out) {
+  char* end = nullptr;
+  out = std::strtod(s, &end);
+  return end != s && *end == '\0';
+}
+
 // a non-negative decimal integer, the whole string
 bool parse_index(const std::string& s, int& out) {
   if (s.empty() || s.size() > 6 || s.find_first_not_of("0123456789") != std::string::npos)
@@ -107,20 +128,24 @@ int main(int argc, char** argv) {
     if (k == "--scene") scene = v;
     else if (k == "--scene-file") scene_path = v;
     else if (k == "--save-scene") save_path = v;
-    else if (k == "--width") width = std::atoi(v), set_w = true;
-    else if (k == "--height") height = std::atoi(v), set_h = true;
-    else if (k == "--spp") spp = std::atoi(v), set_spp = true;
-    else if (k == "--depth") depth = std::atoi(v), set_depth = true;
-    else if (k == "--seed") seed = std::strtoull(v, nullptr, 10), set_seed = true;
+    else if (k == "--width") { if (!parse_int(v, width)) return usage(); set_w = true; }
+    else if (k == "--height") { if (!parse_int(v, height)) return usage(); set_h = true; }
+    else if (k == "--spp") { if (!parse_int(v, spp)) return usage(); set_spp = true; }
+    else if (k == "--depth") { if (!parse_int(v, depth)) return usage(); set_depth = true; }
+    else if (k == "--seed") { if (!parse_u64(v, seed)) return usage(); set_seed = true; }
     else if (k == "-o") out_path = v;
     else if (k == "--accum") accum_path = v;
-    else if (k == "--aperture") aperture = std::atof(v);
-    else if (k == "--focus") focus = std::atof(v);
+    else if (k == "--aperture") { if (!parse_double(v, aperture)) return usage(); }
+    else if (k == "--focus") { if (!parse_double(v, focus)) return usage(); }
     else if (k == "--devices") {
       if (!parse_devices(v, devices)) return usage();
     }
     else if (k == "--rows") {
-      if (std::sscanf(v, "%d:%d", &row_off, &row_stride) != 2) return usage();
+      const std::string r = v;
+      const size_t c = r.find(':');
+      if (c == std::string::npos || !parse_int(r.substr(0, c).c_str(), row_off) ||
+          !parse_int(r.substr(c + 1).c_str(), row_stride))
+        return usage();
     } else return usage();
   }
 
