@@ -40,9 +40,6 @@ constexpr int kHitPrio = 2;
 constexpr int kTailPrio = 1;
 // Minimum waves per SIMD asked of the register allocator (80 VGPRs).
 constexpr int kTraceWaves = 6;
-#ifndef PSRT_LDS_TRIALS
-#define PSRT_LDS_TRIALS 0  // the trial queue in LDS (measurement build; pair with 768-thread blocks)
-#endif
 // Loop schedule (tuned; re-swept under multi-frame launches in r03,
 // profiles/r03_knobs): compile-time constants, so they take no SGPRs in the
 // loop (held as kernel arguments they pushed SGPRs into VGPR-lane spills).
@@ -828,16 +825,8 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
   bool sc_wait = false;  // hit resolved (pbi, pbt), scatter waits for a queued trial
   // look-ahead of random_in_unit_sphere (vec3.h:83-95): accepted trials, in
   // stream order, as raw rand() triples (z, y, x draw order)
-#if PSRT_LDS_TRIALS
-  // the queue as a two-slot ring per lane in LDS, [slot][x, y, z][thread]
-  // (component-major: a wave's 64 lanes hit 64 consecutive words)
-  __shared__ uint32_t s_q[2 * 3 * kTraceBlock];
-  uint32_t* const qp = s_q + threadIdx.x;
-  unsigned qhead = 0, qcnt = 0;  // the oldest trial's slot; trials queued (0..2)
-#else
   uint32_t q0x = 0, q0y = 0, q0z = 0, q1x = 0, q1y = 0, q1z = 0;
   bool qv0 = false, qv1 = false;  // slot 0 / slot 1 of the queue hold a trial
-#endif
   double pbt = 0.0;      // closest t / index so far of this ray's world.hit
   int pbi = -1;
   CullStatsT<kCount> cs{};
@@ -902,13 +891,8 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
           kk = (unsigned short)(k < kSampleKCap ? k : kSampleKCap);
         }
         const unsigned u = su;  // < total < 2^32
-#if PSRT_TEMPORAL_RECORDS  // measurement build (write-traffic A/B, profiles/r05_writes)
-        samples[u] = tt;
-        ((unsigned short*)(samples + total))[u] = kk;
-#else
         __builtin_nontemporal_store(tt, samples + u);
         __builtin_nontemporal_store(kk, (unsigned short*)(samples + total) + u);
-#endif
         done = false;
       }
     }
@@ -982,11 +966,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
           A = (dx * dx + dy * dy) + dz * dz;
           k = 0;
           hint = -1;
-#if PSRT_LDS_TRIALS
-          qcnt = 0;  // the sample's stream starts here: no look-ahead yet
-#else
           qv0 = qv1 = false;  // the sample's stream starts here: no look-ahead yet
-#endif
           active = true;
         }
       }
@@ -1119,11 +1099,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
       // take it (their stream advances), so the draws stay in stream order
       int f = 0;
       do {
-#if PSRT_LDS_TRIALS
-        const bool go = can_fill && qcnt < 2;
-#else
         const bool go = can_fill && !qv1;
-#endif
         if (go) clk.util(kUTrial);
         uint32_t z, y, x;
         uint64_t nxt;
@@ -1131,53 +1107,30 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
         const bool in = in_unit_sphere_raw_f32(x, y, z);  // FP64 only near the surface
         rng = go ? nxt : rng;
         const bool push = go && in;
-#if PSRT_LDS_TRIALS
-        if (push) {
-          uint32_t* const w = qp + ((qhead + qcnt) & 1u) * (3 * kTraceBlock);
-          w[0] = x, w[kTraceBlock] = y, w[2 * kTraceBlock] = z;
-          ++qcnt;
-        }
-#else
         const bool to0 = push && !qv0, to1 = push && qv0;
         q0x = to0 ? x : q0x, q0y = to0 ? y : q0y, q0z = to0 ? z : q0z;
         q1x = to1 ? x : q1x, q1y = to1 ? y : q1y, q1z = to1 ? z : q1z;
         qv1 = qv1 || to1;
         qv0 = qv0 || to0;
-#endif
         ++f;
       } while (f < kRngFill ||
                (f < kRngFill + kRngExtra &&
-#if PSRT_LDS_TRIALS
-                __ballot(want && qcnt == 0) != 0));
-#else
                 __ballot(want && !qv0) != 0));
-#endif
     }
     clk.mark(kSecFillShade);
 
     // ---- scatter: target = (p + n) + random_in_hemisphere(n)  (main.cc:42-43) ----
-#if PSRT_LDS_TRIALS
-    const bool have = qcnt > 0;
-#else
     const bool have = qv0;
-#endif
     sc_wait = want && !have;
     PSRT_ABLATE_AT(SCATTER);
     if (want && have) {
       clk.util(kUScatter);
       const HitRec h = hit_record_of(sv.geo(hit), sv.inv(hit), t, ox, oy, oz, dx, dy, dz);
       // vec3.h:78-81 random(-1, 1) from the queued draws; vec3.h:102-109 flip
-#if PSRT_LDS_TRIALS
-      const uint32_t* const r = qp + qhead * (3 * kTraceBlock);
-      double rx = pm1_raw(r[0]), ry = pm1_raw(r[kTraceBlock]), rz = pm1_raw(r[2 * kTraceBlock]);
-      qhead ^= 1u;
-      --qcnt;
-#else
       double rx = pm1_raw(q0x), ry = pm1_raw(q0y), rz = pm1_raw(q0z);
       q0x = q1x, q0y = q1y, q0z = q1z;
       qv0 = qv1;
       qv1 = false;
-#endif
       if (!((rx * h.nx + ry * h.ny) + rz * h.nz > 0.0)) rx = -rx, ry = -ry, rz = -rz;
       dx = ((h.px + h.nx) + rx) - h.px;
       dy = ((h.py + h.ny) + ry) - h.py;
