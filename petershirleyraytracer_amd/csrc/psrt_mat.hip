@@ -605,20 +605,57 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce_rgb(ReduceArgs a) {
     }
     if (threadIdx.x < kQueues) a.heads[kShardStride * threadIdx.x] = 0ull;
   }
-  const unsigned q = blockIdx.x * kReduceBlock + threadIdx.x;
-  if (q >= a.pixels) return;
+  // One wave per 64 pixels. The 64 pixels' records are one contiguous run
+  // ([pixel][s_count][3] doubles), so the wave stages tiles of kRgbTile
+  // samples per pixel through LDS: 16-B loads spread over the lanes
+  // (consecutive lanes, consecutive 16-B pieces of a pixel's tile), not one
+  // 8-B load per lane per value at a pixel-run stride; then each lane adds its
+  // pixel's samples in order (main.cc:77-84).
+  constexpr unsigned kRgbTile = 8, kRow = kRgbTile * 3 + 1;  // doubles per LDS row (+1: banks)
+  __shared__ double s_c[kReduceBlock * kRow];
+  const unsigned lane = threadIdx.x;
+  const unsigned q0 = blockIdx.x * kReduceBlock;
+  const unsigned q = q0 + lane;
+  const unsigned S = (unsigned)a.s_count;
+  const unsigned np = min((unsigned)kReduceBlock, a.pixels > q0 ? a.pixels - q0 : 0u);
   double r = 0.0, g = 0.0, b = 0.0;
-  if (!a.first_chunk) {
+  if (!a.first_chunk && q < a.pixels) {
     r = a.accum[(size_t)q * 3 + 0];
     g = a.accum[(size_t)q * 3 + 1];
     b = a.accum[(size_t)q * 3 + 2];
   }
-  const double* __restrict__ c = a.samp_t + (size_t)q * a.s_count * 3;
-  for (int s = 0; s < a.s_count; ++s) {
-    r += c[3 * s + 0];
-    g += c[3 * s + 1];
-    b += c[3 * s + 2];
+  const double* __restrict__ run = a.samp_t + (size_t)q0 * S * 3;
+  for (unsigned s0 = 0; s0 < S; s0 += kRgbTile) {
+    const unsigned T = min(kRgbTile, S - s0);
+    const unsigned per = 3 * T;  // doubles of one pixel's tile
+    __syncthreads();
+    if (S % 2 == 0 && T % 2 == 0 && ((uintptr_t)run & 15u) == 0) {
+      // 16-B pieces: pixel p's tile starts 16-B aligned (the run is, and S * 3
+      // and s0 * 3 are even)
+      const unsigned pieces = per / 2;
+      for (unsigned e = lane; e < np * pieces; e += kReduceBlock) {
+        const unsigned p = e / pieces, j = (e - p * pieces) * 2;
+        const double2 v = *(const double2*)(run + (size_t)p * S * 3 + s0 * 3 + j);
+        s_c[p * kRow + j] = v.x;
+        s_c[p * kRow + j + 1] = v.y;
+      }
+    } else {
+      for (unsigned e = lane; e < np * per; e += kReduceBlock) {
+        const unsigned p = e / per, j = e - p * per;
+        s_c[p * kRow + j] = run[(size_t)p * S * 3 + s0 * 3 + j];
+      }
+    }
+    __syncthreads();
+    if (q < a.pixels) {
+      const double* c = s_c + lane * kRow;
+      for (unsigned j = 0; j < T; ++j) {
+        r += c[3 * j + 0];
+        g += c[3 * j + 1];
+        b += c[3 * j + 2];
+      }
+    }
   }
+  if (q >= a.pixels) return;
   if (a.accum) {
     a.accum[(size_t)q * 3 + 0] = r;
     a.accum[(size_t)q * 3 + 1] = g;
