@@ -40,10 +40,6 @@ constexpr int kHitPrio = 2;
 constexpr int kTailPrio = 1;
 // Minimum waves per SIMD asked of the register allocator (80 VGPRs).
 constexpr int kTraceWaves = 6;
-#ifndef PSRT_DRAIN_WALK
-#define PSRT_DRAIN_WALK 0
-#endif
-constexpr bool kDrainWalk = PSRT_DRAIN_WALK;  // walk parked rays at once in the launch's drain
 // Loop schedule (tuned; re-swept under multi-frame launches in r03,
 // profiles/r03_knobs): compile-time constants, so they take no SGPRs in the
 // loop (held as kernel arguments they pushed SGPRs into VGPR-lane spills).
@@ -1056,19 +1052,14 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
     if constexpr (kBVH) {
       const uint64_t pend = __ballot(pending);
       const uint64_t movable = __ballot(active && !pending);
-      // Once the wave's work window is exhausted (the launch's drain) its last
-      // paths' latency, not the SIMD's throughput, decides when it ends: a
-      // parked ray walks at once, to its end, instead of waiting for a batch
-      if (pend != 0 && ((unsigned)__popcll(pend) >= kWalkBatch || movable == 0 ||
-                        (kDrainWalk && exhausted))) {
+      if (pend != 0 && ((unsigned)__popcll(pend) >= kWalkBatch || movable == 0)) {
         __builtin_amdgcn_s_setprio(kWalkPrio);
         if (pending) {
           clk.util(kUWalk);
           PSRT_ABLATE_AT(WALK);
           hit_traverse<kStamps, kLds>(bv, nodes, lleaf, sv, hint, ox, oy,
                                                          oz, dx, dy, dz, A, pbt, pbi, cs, wnode,
-                                                         movable && !(kDrainWalk && exhausted)
-                                                             ? kWalkTail : 0u, (double)wt0);
+                                                         movable ? kWalkTail : 0u, (double)wt0);
           if (wnode >= bv.n_nodes) {
             pending = false;
             resolved = true;

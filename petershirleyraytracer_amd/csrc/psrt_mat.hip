@@ -43,9 +43,6 @@ constexpr double kTmin = 0.001;
 // the dependency-light scatter fills the gaps. Book scene: 2.58 -> 2.49 ms
 // per frame (r04, profiles/r04_mat/ab.txt); two BVH nodes per walk trip
 // were slower here (2.72 ms) and are not used.
-#ifndef PSRT_DRAIN_WALK
-#define PSRT_DRAIN_WALK 0
-#endif
 constexpr int kMatHitPrio = 2;
 constexpr int kMatWalkPrio = 3;
 
@@ -436,9 +433,7 @@ __global__ __launch_bounds__(kMatBlock, kMatWaves) void psrt_trace_mat(const dou
     }
     if constexpr (kBVH) {
       const uint64_t pend = __ballot(pending);
-      // in the launch's drain (the wave's work window exhausted) a parked ray
-      // walks at once: its path's latency decides the launch's end
-      if (pend != 0 && ((unsigned)__popcll(pend) >= a.batch || (PSRT_DRAIN_WALK && exhausted) ||
+      if (pend != 0 && ((unsigned)__popcll(pend) >= a.batch ||
                         __ballot(active && !pending && !fin) == 0)) {
         __builtin_amdgcn_s_setprio(kMatWalkPrio);
         if (pending) {
