@@ -1,0 +1,62 @@
+"""Every tuning knob keeps the output bit-identical (include/rt.h, "tuning"):
+the final scene and the book scene rendered under each knob's non-default
+settings equal the default frame and its ray count. The knobs change work
+distribution (queue shape, tickets, residency), which shortcuts run (LDS
+staging, fixed-point exit, big-sphere class, walk batch) or when structures
+are rebuilt; none may change a bit."""
+import numpy as np
+import pytest
+
+from conftest import bits
+
+import petershirleyraytracer_amd as P
+from petershirleyraytracer_amd.render import LensCamera
+
+pytestmark = pytest.mark.gpu
+
+TRACE_KNOBS = [
+    ("queue_k", 1), ("queue_k", 5), ("queue_d", 1), ("queue_d", 8),
+    ("no_fixpoint", 1), ("no_lds", 1), ("no_camlist", 1), ("no_neighbors", 1),
+    ("blocks_per_cu", 1), ("blocks_per_cu", 2), ("big_ratio", 3), ("big_ratio", 64),
+    ("scene_rebuild", 1), ("flush_at", 1000),
+]
+MAT_KNOBS = [("mat_batch", 1), ("mat_batch", 64), ("mat_lds", 0), ("queue_k", 5),
+             ("big_ratio", 3), ("no_camlist", 1)]
+
+
+@pytest.fixture(scope="module")
+def c3_default(final_scene):
+    cam = P.camera_look_at(aspect=96 / 64)
+    acc, rgb, st = P.render(final_scene, cam, 96, 64, 8, seed=11)
+    return cam, acc, rgb, st
+
+
+@pytest.mark.parametrize("name,value", TRACE_KNOBS)
+def test_trace_knob_is_bit_neutral(final_scene, c3_default, knobs, name, value):
+    cam, want, wrgb, ws = c3_default
+    knobs(name, value)
+    acc, rgb, st = P.render(final_scene, cam, 96, 64, 8, seed=11)
+    assert np.array_equal(bits(acc), bits(want)) and np.array_equal(rgb, wrgb), name
+    assert st["rays"] == ws["rays"], name
+
+
+def test_linear_chunk_is_bit_neutral(oracle_mod, knobs):
+    """The small-scene (no BVH) path's queue ticket."""
+    two = P.scene_two_spheres()
+    cam = P.camera_default()
+    want, _, rays = oracle_mod.render(two, cam, 80, 45, 6, threads=8)
+    for chunk in (64, 256, 4096):
+        knobs("linear_chunk", chunk)
+        acc, _, st = P.render(two, cam, 80, 45, 6)
+        assert np.array_equal(bits(acc), bits(want)) and st["rays"] == rays, chunk
+
+
+@pytest.mark.parametrize("name,value", MAT_KNOBS)
+def test_material_knob_is_bit_neutral(oracle_mod, knobs, name, value):
+    sp, mt = oracle_mod.scene_book_final(1)
+    lens = oracle_mod.camera_look_at_lens(aspect=1.5)
+    lc = LensCamera(lens["base"], lens["u"], lens["v"], lens["lens_radius"])
+    want, _, ws = P.render_materials(sp, mt, lc, 72, 48, 4, 50, 9)
+    knobs(name, value)
+    acc, _, st = P.render_materials(sp, mt, lc, 72, 48, 4, 50, 9)
+    assert np.array_equal(bits(acc), bits(want)) and st["rays"] == ws["rays"], name
