@@ -43,9 +43,6 @@ constexpr double kTmin = 0.001;
 // the dependency-light scatter fills the gaps. Book scene: 2.58 -> 2.49 ms
 // per frame (r04, profiles/r04_mat/ab.txt); two BVH nodes per walk trip
 // were slower here (2.72 ms) and are not used.
-#ifndef PSRT_MAT_PREFETCH
-#define PSRT_MAT_PREFETCH 0
-#endif
 constexpr int kMatHitPrio = 2;
 constexpr int kMatWalkPrio = 3;
 
@@ -201,29 +198,9 @@ __device__ __forceinline__ void hit_walk_m(TestCount<kCount>& nt, TestCount<kCou
   // until every lane of the wave holds one or is done; the held leaves' FP64
   // tests then run together instead of once per trip in which any lane has one.
   int node = bv.walk0;  // the root is not tested (psrt_kernels.h BvhView::walk0)
-#if PSRT_MAT_PREFETCH
-  // Both successors of a node (node + 1 on an interior hit, skip otherwise)
-  // are read before its slab test, so the next trip's node is in registers
-  // when the test decides: the walk's dependent LDS reads overlap the test
-  // instead of following it. Node n_nodes is the padding node: node + 1 and
-  // skip (<= n_nodes) are always readable.
-  float4 n0 = nodes[2 * node], n1 = nodes[2 * node + 1];
-#endif
   for (;;) {
     int leaf = -1;
     while (node < bv.n_nodes && leaf < 0) {
-#if PSRT_MAT_PREFETCH
-      const int skip = __float_as_int(n1.z), lf = __float_as_int(n1.w);
-      const float4 a0 = nodes[2 * node + 2], a1 = nodes[2 * node + 3];
-      const float4 s0 = nodes[2 * skip], s1 = nodes[2 * skip + 1];
-      nb.add(1u);
-      const bool hit = slab_hit(n0, n1, ix, iy, iz, oix, oiy, oiz, tlo, tmax);
-      const bool go_in = hit && lf < 0;  // interior hit: DFS order continues at node + 1
-      if (hit && lf >= 0) leaf = lf;
-      node = go_in ? node + 1 : skip;
-      n0 = go_in ? a0 : s0;
-      n1 = go_in ? a1 : s1;
-#else
       const float4 n0 = nodes[2 * node], n1 = nodes[2 * node + 1];
       const int skip = __float_as_int(n1.z), lf = __float_as_int(n1.w);
       nb.add(1u);
@@ -235,7 +212,6 @@ __device__ __forceinline__ void hit_walk_m(TestCount<kCount>& nt, TestCount<kCou
         leaf = lf;
         node = skip;
       }
-#endif
     }
     if (leaf < 0) break;
     const int first = leaf >> 8, cnt = leaf & 255;
