@@ -15,6 +15,7 @@
 //   raytracer --scene final --save-scene final.scene   # write the scene, render nothing
 //   raytracer --scene book --width 1200 --height 800 --spp 10 [--aperture 0.1 --focus 10]
 //                                   # the book's materials + thin lens
+#include <cerrno>
 #include <chrono>
 #include <cstdio>
 #include <climits>
@@ -60,25 +61,28 @@ int usage() {
   return 2;
 }
 
-// --devices: "N" = devices 0..N-1; "a,b,c" = those members (repeats allowed)
-// a decimal integer / a floating-point number, the whole string
+// a decimal integer / an unsigned 64-bit integer / a floating-point number,
+// the whole string, in range
 bool parse_int(const char* s, int& out) {
   char* end = nullptr;
+  errno = 0;
   const long v = std::strtol(s, &end, 10);
-  if (end == s || *end != '\0' || v < INT_MIN || v > INT_MAX) return false;
+  if (end == s || *end != '\0' || errno == ERANGE || v < INT_MIN || v > INT_MAX) return false;
   out = (int)v;
   return true;
 }
 bool parse_u64(const char* s, unsigned long long& out) {
   char* end = nullptr;
   if (*s == '-') return false;
+  errno = 0;
   out = std::strtoull(s, &end, 10);
-  return end != s && *end == '\0';
+  return end != s && *end == '\0' && errno != ERANGE;
 }
 bool parse_double(const char* s, double& out) {
   char* end = nullptr;
+  errno = 0;
   out = std::strtod(s, &end);
-  return end != s && *end == '\0';
+  return end != s && *end == '\0' && errno != ERANGE;
 }
 
 // a non-negative decimal integer, the whole string
