@@ -65,10 +65,21 @@ inline void check(int rc, const char* what) {
   if (rc != RT_OK) throw std::runtime_error(std::string(what) + ": " + rt_last_error());
 }
 
+// The structs of this header (rt_stats grew in ABI 5) must be the loaded
+// library's: a libpsrt.so of another RT_ABI_VERSION is refused before any
+// call could write past a caller's struct.
+inline void check_abi() {
+  static const int v = rt_abi_version();
+  if (v != RT_ABI_VERSION)
+    throw std::runtime_error("libpsrt.so ABI version " + std::to_string(v) + ", header " +
+                             std::to_string(RT_ABI_VERSION));
+}
+
 // main.cc:72-88 for output rows row_offset, row_offset+row_stride, ...
 inline frame render(const hittable_list& world, const camera& cam, int width, int height,
                     int spp, int max_depth, uint64_t seed = 0, int row_offset = 0,
                     int row_stride = 1) {
+  check_abi();
   const std::vector<rt_sphere> spheres = flatten(world);
   const rt_camera c = to_rt(cam);
   rt_params p{};
@@ -103,6 +114,7 @@ inline frame render(const hittable_list& world, const camera& cam, int width, in
 class device_group {
  public:
   explicit device_group(const std::vector<int>& devices) {
+    check_abi();
     check(rt_group_create(devices.data(), (int)devices.size(), &g_), "rt_group_create");
   }
   ~device_group() { rt_group_destroy(g_); }
@@ -157,6 +169,7 @@ inline frame render_materials(const std::vector<rt_sphere>& spheres,
                               const std::vector<rt_material>& mats, const rt_camera_lens& cam,
                               int width, int height, int spp, int max_depth, uint64_t seed = 0,
                               int row_offset = 0, int row_stride = 1) {
+  check_abi();
   if (mats.size() != spheres.size())
     throw std::runtime_error("render_materials: one material per sphere");
   rt_params p{};

@@ -11,6 +11,10 @@ import os
 from .build import LIB
 
 RT_OK = 0
+# include/rt.h RT_ABI_VERSION: the struct layouts below (RtStats grew in ABI 5)
+# are that version's, so a library of another version is refused at load
+# (tests/test_abi.py checks this constant against the header)
+ABI_VERSION = 5
 ERRORS = {-1: "RT_E_INVALID", -2: "RT_E_HIP", -3: "RT_E_NODEVICE", -4: "RT_E_NOMEM",
           -5: "RT_E_SCENE"}
 
@@ -153,6 +157,9 @@ def load(build_if_missing: bool = False):
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
+    if L.rt_abi_version() != ABI_VERSION:
+        raise RtError(f"{lib_path}: ABI version {L.rt_abi_version()}, this binding is "
+                      f"{ABI_VERSION} (include/rt.h RT_ABI_VERSION)")
     _lib = L
     return L
 

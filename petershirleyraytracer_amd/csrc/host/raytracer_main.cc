@@ -15,6 +15,7 @@
 //   raytracer --scene final --save-scene final.scene   # write the scene, render nothing
 //   raytracer --scene book --width 1200 --height 800 --spp 10 [--aperture 0.1 --focus 10]
 //                                   # the book's materials + thin lens
+#include <cctype>
 #include <cerrno>
 #include <chrono>
 #include <cstdio>
@@ -73,7 +74,9 @@ bool parse_int(const char* s, int& out) {
 }
 bool parse_u64(const char* s, unsigned long long& out) {
   char* end = nullptr;
-  if (*s == '-') return false;
+  // digits only: strtoull would skip leading blanks and accept a sign, and
+  // wrap " -1" to 2^64 - 1
+  if (!std::isdigit((unsigned char)*s)) return false;
   errno = 0;
   out = std::strtoull(s, &end, 10);
   return end != s && *end == '\0' && errno != ERANGE;

@@ -108,19 +108,30 @@ struct Tuning {
 
 namespace {
 
+// Each knob's valid range: every later use casts the value to an integer type
+// or multiplies it into a size, so rt_context_set_tuning rejects anything
+// outside [lo, hi] (RT_E_INVALID) instead of letting a cast wrap.
 struct TuningKey {
   const char* name;
   double psrt::Tuning::*field;
+  double lo, hi;
 };
 const TuningKey kTuningKeys[] = {
-    {"sample_buf_mb", &psrt::Tuning::sample_buf_mb}, {"queue_k", &psrt::Tuning::queue_k},
-    {"queue_d", &psrt::Tuning::queue_d},             {"linear_chunk", &psrt::Tuning::linear_chunk},
-    {"no_camlist", &psrt::Tuning::no_camlist},       {"no_neighbors", &psrt::Tuning::no_neighbors},
-    {"no_fixpoint", &psrt::Tuning::no_fixpoint},     {"no_lds", &psrt::Tuning::no_lds},
-    {"blocks_per_cu", &psrt::Tuning::blocks_per_cu}, {"mat_lds", &psrt::Tuning::mat_lds},
-    {"mat_batch", &psrt::Tuning::mat_batch},         {"flush_at", &psrt::Tuning::flush_at},
-    {"stamps", &psrt::Tuning::stamps},               {"scene_rebuild", &psrt::Tuning::scene_rebuild},
-    {"big_ratio", &psrt::Tuning::big_ratio},
+    {"sample_buf_mb", &psrt::Tuning::sample_buf_mb, 1, 1 << 22},  // 1 MiB .. 4 TiB
+    {"queue_k", &psrt::Tuning::queue_k, 0, 64},
+    {"queue_d", &psrt::Tuning::queue_d, 0.125, 64},
+    {"linear_chunk", &psrt::Tuning::linear_chunk, 0, 1 << 20},
+    {"no_camlist", &psrt::Tuning::no_camlist, 0, 1},
+    {"no_neighbors", &psrt::Tuning::no_neighbors, 0, 1},
+    {"no_fixpoint", &psrt::Tuning::no_fixpoint, 0, 1},
+    {"no_lds", &psrt::Tuning::no_lds, 0, 1},
+    {"blocks_per_cu", &psrt::Tuning::blocks_per_cu, 0, 64},
+    {"mat_lds", &psrt::Tuning::mat_lds, -1, 1},
+    {"mat_batch", &psrt::Tuning::mat_batch, 1, 64},
+    {"flush_at", &psrt::Tuning::flush_at, 0, 4294967295.0},
+    {"stamps", &psrt::Tuning::stamps, 0, 1},
+    {"scene_rebuild", &psrt::Tuning::scene_rebuild, 0, 1},
+    {"big_ratio", &psrt::Tuning::big_ratio, 0, 1e300},
 };
 std::mutex g_tuning_mu;
 psrt::Tuning g_tuning;  // the process defaults (rt_context_set_tuning(NULL, ...))
@@ -156,6 +167,7 @@ struct rt_context {
   uint4* d_cell_rec = nullptr;  // grid lists as inline records (BvhHost::cell_rec)
   uint2* d_nb_rec = nullptr;    // neighbour lists as inline records (BvhHost::nb_rec)
   std::vector<rt_sphere> scene;   // the scene the structures were built for
+  double built_big_ratio = 0;     // Tuning::big_ratio the structures were built with
   psrt::GridHost pgrid;  // point-location grid (host copy of the geometry)
   double pad = 0.0;
   int n_nodes = 0, n_big = 0, n_leaf = 0;
@@ -436,7 +448,7 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
   // the culling structures, only the camera changes (its lists are rebuilt).
   if (n == c->n && n > 0 && (size_t)n == c->scene.size() &&
       std::memcmp(c->scene.data(), sph, (size_t)n * sizeof(rt_sphere)) == 0 &&
-      !c->tune.scene_rebuild) {
+      !c->tune.scene_rebuild && c->tune.big_ratio == c->built_big_ratio) {
     c->cam = *cam;
     c->plist_valid = false;
     return RT_OK;
@@ -553,6 +565,7 @@ int rt_context_set_scene(rt_context* c, const rt_sphere* sph, int n, const rt_ca
   // renders on any other stream too
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->scene.assign(sph, sph + n);
+  c->built_big_ratio = c->tune.big_ratio;
   return RT_OK;
 }
 
@@ -610,6 +623,10 @@ static int check_params(const rt_params* p) {
     return set_error(RT_E_INVALID, "max_depth %d above %d with RT_FLAG_MATERIALS", p->max_depth,
                      psrt::kMatMaxDepth);
   return RT_OK;
+}
+
+extern "C++" {  // psrt_error.h (rt_group_render's check)
+int psrt::check_render_params(const void* p) { return check_params((const rt_params*)p); }
 }
 
 // Guided work queue (psrt_kernels.h TraceArgs::ph_*), BVH scenes. The first
@@ -1467,6 +1484,9 @@ int rt_context_set_tuning(rt_context* c, const char* name, double value) {
     if (std::strcmp(k.name, name) != 0) continue;
     if (!std::isfinite(value))
       return set_error(RT_E_INVALID, "rt_context_set_tuning: %s must be finite", name);
+    if (value < k.lo || value > k.hi)
+      return set_error(RT_E_INVALID, "rt_context_set_tuning: %s = %g outside [%g, %g]", name, value,
+                       k.lo, k.hi);
     if (c) {
       c->tune.*k.field = value;
     } else {

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstring>
 #include <exception>
 #include <string>
@@ -147,11 +148,18 @@ int rt_group_set_scene(rt_group* grp, const rt_sphere* sph, int n, const rt_came
   std::vector<int> rc(grp->m.size(), RT_OK);
   std::vector<std::string> err(grp->m.size());
   std::vector<std::thread> th;
-  for (size_t g = 0; g < grp->m.size(); ++g)
-    th.emplace_back([&, g] {
-      rc[g] = rt_context_set_scene(grp->m[g].ctx, sph, n, cam);
-      if (rc[g]) err[g] = rt_last_error();
-    });
+  th.reserve(grp->m.size());
+  try {
+    for (size_t g = 0; g < grp->m.size(); ++g)
+      th.emplace_back([&, g] {
+        rc[g] = rt_context_set_scene(grp->m[g].ctx, sph, n, cam);
+        if (rc[g]) err[g] = rt_last_error();
+      });
+  } catch (const std::exception& e) {
+    for (auto& t : th) t.join();
+    return psrt::set_error(RT_E_NOMEM, "rt_group_set_scene: cannot start a member thread: %s",
+                           e.what());
+  }
   for (auto& t : th) t.join();
   for (size_t g = 0; g < rc.size(); ++g)
     if (rc[g]) return psrt::set_error(rc[g], "member %zu: %s", g, err[g].c_str());
@@ -161,26 +169,39 @@ int rt_group_set_scene(rt_group* grp, const rt_sphere* sph, int n, const rt_came
 int rt_group_render(rt_group* grp, const rt_params* p, double* accum_rgb, unsigned char* rgb8,
                     rt_stats* stats) {
   if (!grp || !p) return psrt::set_error(RT_E_INVALID, "rt_group_render: bad arguments");
+  // the members' own renders would check these too, but only after their
+  // shard arithmetic and buffer sizing ran on the unchecked values
+  int prc = psrt::check_render_params(p);
+  if (prc) return prc;
   if (p->flags & RT_FLAG_MATERIALS)
     return psrt::set_error(RT_E_INVALID, "rt_group_render: RT_FLAG_MATERIALS is not supported");
-  if (p->row_stride < 1 || p->row_offset < 0)
-    return psrt::set_error(RT_E_INVALID, "rt_group_render: bad shard");
+  const int G = (int)grp->m.size();
+  if ((long long)p->row_stride * G > INT_MAX ||
+      (long long)p->row_offset + (long long)(G - 1) * p->row_stride > INT_MAX)
+    return psrt::set_error(RT_E_INVALID, "rt_group_render: row_stride %d x %d members overflows",
+                           p->row_stride, G);
   if (!accum_rgb && !rgb8 && rt_rows_owned(p->height, p->row_offset, p->row_stride) > 0)
     return psrt::set_error(RT_E_INVALID, "rt_group_render: no output buffer");
-  const int G = (int)grp->m.size();
   std::vector<int> rc(G, RT_OK);
   std::vector<std::string> err(G);
   std::vector<rt_stats> st(G);
   std::vector<std::thread> th;
-  for (int g = 0; g < G; ++g)
-    th.emplace_back([&, g] {
-      try {
-        rc[g] = member_render(grp->m[g], g, G, *p, accum_rgb, rgb8, &st[g]);
-      } catch (const std::exception& e) {
-        rc[g] = psrt::set_error(RT_E_HIP, "%s", e.what());
-      }
-      if (rc[g]) err[g] = rt_last_error();
-    });
+  th.reserve(G);
+  try {
+    for (int g = 0; g < G; ++g)
+      th.emplace_back([&, g] {
+        try {
+          rc[g] = member_render(grp->m[g], g, G, *p, accum_rgb, rgb8, &st[g]);
+        } catch (const std::exception& e) {
+          rc[g] = psrt::set_error(RT_E_HIP, "%s", e.what());
+        }
+        if (rc[g]) err[g] = rt_last_error();
+      });
+  } catch (const std::exception& e) {  // std::system_error: no thread for a member
+    for (auto& t : th) t.join();
+    return psrt::set_error(RT_E_NOMEM, "rt_group_render: cannot start a member thread: %s",
+                           e.what());
+  }
   for (auto& t : th) t.join();
   for (int g = 0; g < G; ++g)
     if (rc[g]) return psrt::set_error(rc[g], "member %d: %s", g, err[g].c_str());

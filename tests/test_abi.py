@@ -36,7 +36,9 @@ def test_exports_every_declared_symbol():
 
 def test_abi_version_and_info():
     L = _lib.load()
-    assert L.rt_abi_version() == 5
+    hdr = open(os.path.join(ROOT, "include", "rt.h")).read()
+    want = int(re.search(r"#define RT_ABI_VERSION (\d+)", hdr).group(1))
+    assert L.rt_abi_version() == want == _lib.ABI_VERSION == 5
     assert b"gfx950" in L.rt_build_info()
 
 
@@ -164,6 +166,16 @@ def test_tuning_knobs_without_device():
         P.set_tuning("no_such_knob", 1)
     with pytest.raises(_lib.RtError, match="finite"):
         P.set_tuning("queue_k", float("nan"))
+    # every knob has a range: values whose integer casts would wrap are errors
+    # and leave the old value in place
+    for name, bad in (("sample_buf_mb", 1e20), ("sample_buf_mb", 0.5), ("queue_k", -1),
+                      ("blocks_per_cu", -2), ("mat_batch", 1e12), ("flush_at", -5),
+                      ("flush_at", 2.0 ** 40), ("linear_chunk", -1), ("no_lds", 2),
+                      ("big_ratio", -1)):
+        before = P.get_tuning(name)
+        with pytest.raises(_lib.RtError, match="outside"):
+            P.set_tuning(name, bad)
+        assert P.get_tuning(name) == before, name
 
 
 def test_render_path_reads_no_environment():

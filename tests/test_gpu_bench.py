@@ -104,3 +104,28 @@ def test_bench_two_ranks_c4_gathered_frame_checked():
     assert par["checked"] is True, par
     assert par["fp64_bit_identical"] is True and par["ranks_covered"] == 2, par
     assert par["spp"] == 500, par
+
+
+def test_bench_eight_ranks_driver_command():
+    """The driver's 8-GPU command (torchrun --nproc-per-node 8 bench.py --gpus 8),
+    rehearsed with 8 ranks on the one GPU over gloo: every
+    rank reports, the gathered frame's sampled rows cover all 8 ranks and match
+    the reference bit for bit, and every rank's timed launch equals its
+    one-frame render. profiles/r06_rehearsal8 holds the C3 and C4 lines."""
+    _require_ref()
+    env = dict(os.environ, PSRT_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1",
+               OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+           "--gpus", "8", "--config", "c1", "--steps", "3", "--warmup", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=200, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 8 and d["scaling"] == "strong" and d["config"]["config_id"] == "c1"
+    assert sorted(p["rank"] for p in d["per_rank"]) == list(range(8))
+    assert sum(p["rows"] for p in d["per_rank"]) == 225
+    par = d["parity_vs_cpu"]
+    assert par["checked"] is True and par["fp64_bit_identical"] is True, par
+    assert par["ranks_covered"] == 8, par
+    bc = d["batch_check"]
+    assert bc["all_ranks_equal"] is True and bc["last_frame_equal"] is True, bc

@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 TRACE_KNOBS = [
     ("queue_k", 1), ("queue_k", 5), ("queue_d", 1), ("queue_d", 8),
     ("no_fixpoint", 1), ("no_lds", 1), ("no_camlist", 1), ("no_neighbors", 1),
-    ("blocks_per_cu", 1), ("blocks_per_cu", 2), ("big_ratio", 3), ("big_ratio", 64),
+    ("blocks_per_cu", 1), ("blocks_per_cu", 2), ("big_ratio", 3), ("big_ratio", 1e4),
     ("scene_rebuild", 1), ("flush_at", 1000),
 ]
 MAT_KNOBS = [("mat_batch", 1), ("mat_batch", 64), ("mat_lds", 0), ("queue_k", 5),
@@ -28,16 +28,25 @@ MAT_KNOBS = [("mat_batch", 1), ("mat_batch", 64), ("mat_lds", 0), ("queue_k", 5)
 def c3_default(final_scene):
     cam = P.camera_look_at(aspect=96 / 64)
     acc, rgb, st = P.render(final_scene, cam, 96, 64, 8, seed=11)
-    return cam, acc, rgb, st
+    _, _, counted = P.render(final_scene, cam, 96, 64, 8, seed=11, cull_stats=True)
+    return cam, acc, rgb, st, counted
 
 
 @pytest.mark.parametrize("name,value", TRACE_KNOBS)
 def test_trace_knob_is_bit_neutral(final_scene, c3_default, knobs, name, value):
-    cam, want, wrgb, ws = c3_default
+    cam, want, wrgb, ws, wcount = c3_default
     knobs(name, value)
     acc, rgb, st = P.render(final_scene, cam, 96, 64, 8, seed=11)
     assert np.array_equal(bits(acc), bits(want)) and np.array_equal(rgb, wrgb), name
     assert st["rays"] == ws["rays"], name
+    if name == "big_ratio":
+        # the knob must reach the structures of an unchanged scene:
+        # ratio 3 adds the three r = 1 spheres to the class tested on every ray,
+        # 1e4 empties it (the ground goes into the BVH); either changes the
+        # executed test counts of the same frame
+        _, _, cnt = P.render(final_scene, cam, 96, 64, 8, seed=11, cull_stats=True)
+        assert (cnt["tests_executed"], cnt["box_tests"]) != (
+            wcount["tests_executed"], wcount["box_tests"]), (name, value)
 
 
 def test_linear_chunk_is_bit_neutral(oracle_mod, knobs):

@@ -93,7 +93,8 @@ def test_host_app_rejects_bad_options(tmp_path):
     out = str(tmp_path / "x.ppm")
     for bad in (["--width", "8x"], ["--devices", "0,x"], ["--devices", "0,,1"], ["--devices", "-1"],
                 ["--devices", "0"], ["--devices", "abc"], ["--scene", "book", "--devices", "2"],
-                ["--rows", "1:2x"], ["--rows", "1"], ["--seed", "-3"], ["--aperture", "0.1q"],
+                ["--rows", "1:2x"], ["--rows", "1"], ["--seed", "-3"], ["--seed", " -1"],
+                ["--seed", "+4"], ["--aperture", "0.1q"],
                 ["--width", "99999999999"], ["--seed", "99999999999999999999999"],
                 ["--focus", "1e999"]):
         r = subprocess.run([exe, *bad, "-o", out, "--width", "8", "--height", "4", "--spp", "1"],
