@@ -103,9 +103,6 @@ struct Tuning {
   double stamps = 0;         // diagnostic kernel variant (section clocks, utilisation probes)
   double scene_rebuild = 0;  // rebuild the culling structures for an unchanged scene
   double big_ratio = 0;      // radius ratio of the big-sphere class (0: psrt_bvh's default)
-  // launch tail: a wave whose queue is empty hands its paths to its workgroup's
-  // other waves once it holds at most this many (TraceArgs::mig_below; 0: off)
-  double mig_below = 16;
 };
 }  // namespace psrt
 
@@ -135,7 +132,6 @@ const TuningKey kTuningKeys[] = {
     {"stamps", &psrt::Tuning::stamps, 0, 1},
     {"scene_rebuild", &psrt::Tuning::scene_rebuild, 0, 1},
     {"big_ratio", &psrt::Tuning::big_ratio, 0, 1e300},
-    {"mig_below", &psrt::Tuning::mig_below, 0, 16},
 };
 std::mutex g_tuning_mu;
 psrt::Tuning g_tuning;  // the process defaults (rt_context_set_tuning(NULL, ...))
@@ -158,7 +154,6 @@ struct rt_context {
   int grid = 0;       // resident blocks of psrt_trace<false>
   int grid_bvh = 0;   // resident blocks of psrt_trace<true>
   unsigned lds_max = 0;  // largest dynamic LDS that keeps grid_bvh resident (staged scenes)
-  unsigned lds_max_lin = 0;  // the same for psrt_trace<false> at grid (the migration pool)
   // exact-culling structure (psrt_bvh.h)
   bool bvh = false;
   float4* d_nodes = nullptr;
@@ -363,20 +358,6 @@ int rt_context_create(int device, rt_context** out) {
         pc >= per_cu) {
       c->lds_max = b;
       break;
-    }
-  }
-  {  // the linear (small-scene) variant keeps its residency up to lds_max_lin
-    int lin = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lin, psrt::psrt_trace<false, false, false, false>,
-                                                          psrt::kTraceBlock, 0));
-    for (unsigned b = 65536; b >= 256; b -= 256) {
-      int pc = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, psrt::psrt_trace<false, false, false, false>,
-                                                       psrt::kTraceBlock, b) == hipSuccess &&
-          pc >= lin) {
-        c->lds_max_lin = b;
-        break;
-      }
     }
   }
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace_mat<false, false, false>,
@@ -1127,22 +1108,12 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     // kernel's resident count otherwise: its global-memory variant)
     const unsigned lds_bytes = psrt::lds_layout(c->n, c->n_nodes, c->n_leaf, c->n_big).bytes;
     const bool lds = use_bvh && lds_bytes <= c->lds_max && !c->tune.no_lds;
-    // the launch tail's path pool (TraceArgs::mig_*) takes the dynamic LDS
-    // the residency leaves after the staged scene: C3 ~2 KB, 16+ records
-    const unsigned scene_bytes = lds ? lds_bytes : 0;
-    const unsigned room = use_bvh ? c->lds_max : c->lds_max_lin;
-    const unsigned slots = room >= scene_bytes + psrt::kMigSlots * psrt::kMigRecord
-                               ? psrt::kMigSlots : 0u;
-    const unsigned below = std::min((unsigned)c->tune.mig_below, slots);
-    ta.mig_slots = below >= 1 ? slots : 0u;
-    ta.mig_below = ta.mig_slots ? below : 0u;
-    ta.mig_off = scene_bytes;
-    const unsigned dyn_bytes = scene_bytes + ta.mig_slots * psrt::kMigRecord;
     // Tuning::blocks_per_cu: measurement knob (occupancy sweep), 0 = resident max
     const int bpc = (int)c->tune.blocks_per_cu;
     auto launch = [&](auto kern, int grid) {
       if (bpc > 0) grid = std::min(grid, std::max(1, c->cus * bpc));
-      hipLaunchKernelGGL(kern, dim3(grid), blk, dyn_bytes, st, g4, ir, c->d_samples, ta, bv);
+      hipLaunchKernelGGL(kern, dim3(grid), blk, lds ? lds_bytes : 0, st, g4, ir, c->d_samples, ta,
+                         bv);
     };
     // RT_FLAG_CULL_STATS: the variant that counts sphere / box tests
     auto pick = [&](auto kBVH, auto kStamps, auto kLds, int grid) {

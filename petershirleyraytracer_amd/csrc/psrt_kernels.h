@@ -115,18 +115,7 @@ struct TraceArgs {
   FastDiv div_s, div_w, div_p;      // unit / s_count, q / width, (f * pixels + q) / pixels
   unsigned flush_at;                // per-lane counters flush to the totals at this value
   int tail_prio;                    // raise the issue priority of waves whose queue is empty
-  // Launch-tail path migration (psrt_trace, DESIGN.md §4 "Launch tail"): once
-  // its work window is exhausted, a wave with 1..mig_below live paths hands
-  // them to the other waves of its workgroup through a pool of mig_slots
-  // path records in dynamic LDS at byte offset mig_off (kMigRecord bytes
-  // each, field-major), then exits; mig_slots = 0 turns migration off.
-  unsigned mig_slots, mig_below, mig_off;
 };
-// bytes of one migrated path's state in the LDS pool (8 doubles, 15 words,
-// padded), and the pool's records (a compile-time count: the pool's word
-// offsets are then instruction immediates)
-constexpr unsigned kMigRecord = 128;
-constexpr unsigned kMigSlots = 16;
 
 // BVH node as the device reads it (two float4, from psrt_bvh.h BvhNode):
 // {lo.x, lo.y, hi.x, hi.y}, {lo.z, hi.z, skip, leaf} (skip / leaf: int bits),

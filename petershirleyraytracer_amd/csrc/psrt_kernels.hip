@@ -55,9 +55,6 @@ constexpr unsigned kWalkBatch = PSRT_WALK_BATCH;  // parked lanes that trigger a
 #define PSRT_WALK_TAIL 6  // r04 re-sweep (profiles/r04_knobs2): 2 / 4 / 6 / 8
 #endif
 constexpr unsigned kWalkTail = PSRT_WALK_TAIL;  // a BVH pass stops once this few lanes still walk
-#ifndef PSRT_MIG_SPLIT
-#define PSRT_MIG_SPLIT 0
-#endif
 #ifndef PSRT_RNG_FILL
 #define PSRT_RNG_FILL 2
 #endif
@@ -711,46 +708,6 @@ __device__ __forceinline__ int world_hit_bvh(const double4* __restrict__ geo, in
 }
 
 
-// ---- launch-tail path migration (TraceArgs::mig_*) ----
-// When the work queue is empty, a wave's iteration costs about the same for
-// 1 live lane as for 64, and the drain's waves share the SIMDs with each
-// other: a wave down to a few paths hands them to the idle lanes of its
-// workgroup's other waves and exits, so the drain runs in fewer, fuller
-// waves. Every pool operation runs under the workgroup's LDS lock:
-//  - take:   an exhausted wave with idle lanes pops paths from the pool;
-//  - donate: a wave with 1..mig_below live paths pushes them all and exits,
-//            only if another wave of the workgroup is still alive and the
-//            pool has room;
-//  - exit:   a wave with no paths leaves only when the pool is empty.
-// So the last wave to leave has emptied the pool: no path is lost. A path's
-// state moves whole (position, direction, bounce count, stream, bounds, the
-// look-ahead queue, a parked walk's resume point); its bits and draws do not
-// depend on the lane that carries it.
-struct MigShared {
-  int lock;   // 0 free, 1 held
-  int count;  // records in the pool
-  int alive;  // waves of the workgroup still in the loop
-  // TraceArgs::mig_slots / mig_below / mig_off, re-read from LDS where used:
-  // held across the loop as kernel arguments they would take SGPRs the loop
-  // spills to VGPR lanes
-  int slots, below, off;
-};
-
-__device__ __forceinline__ void mig_lock(MigShared* m, unsigned lane) {
-  if (lane == 0)
-    while (atomicCAS(&m->lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(2);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-__device__ __forceinline__ void mig_unlock(MigShared* m, unsigned lane) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  if (lane == 0) atomicExch(&m->lock, 0);
-}
-
-__device__ __forceinline__ int mig_read(const int* p) {
-  return __builtin_amdgcn_readfirstlane(*(const volatile int*)p);
-}
-
 // A wave's per-lane 32-bit counters -> one 64-bit atomic each into the
 // block's counter set (psrt_kernels.h TraceArgs::ray_counter: [0] rays,
 // [1] full FP64 sphere tests, [2] box tests, [4] pre-rejects, [5] root-box
@@ -800,10 +757,6 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
   constexpr unsigned kFlushWords = kCount ? 6 : 3;
   __shared__ unsigned long long s_flush[kFlushWords];
   if (threadIdx.x < kFlushWords) s_flush[threadIdx.x] = 0ull;
-  __shared__ MigShared s_mig;
-  if (threadIdx.x == 0)
-    s_mig = MigShared{0, 0, (int)(blockDim.x / 64), (int)a.mig_slots, (int)a.mig_below,
-                      (int)a.mig_off};
   if (threadIdx.x == 0) s_gc = grid_consts(bv);
   if (threadIdx.x < 12)
     s_rc.cam[threadIdx.x] = threadIdx.x < 3   ? a.org[threadIdx.x]
@@ -896,13 +849,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
     }
   }
 
-  // One iteration of the bounce loop. Two copies run: the steady state
-  // without the launch-tail exchange, then (queue empty, pool present) the
-  // drain with it, so the exchange's code is outside the steady-state loop
-  // and its register allocation. Returns 0: next iteration, 1: the wave
-  // leaves, 2: go on in the drain copy.
-  auto step = [&](auto kMigT) -> int {
-    constexpr bool kMigC = decltype(kMigT)::value;
+  for (;;) {
     // ---- finish + refill lanes whose sample ended (wavefront ballot compaction) ----
     // The block runs for the wave once at least refill_min lanes are idle (or
     // none is live): its cost is per wave, so batching finished lanes pays
@@ -1044,80 +991,8 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
         }
       }
     }
-    // ---- launch tail: path migration inside the workgroup (MigShared) ----
-    // The pool (mig_slots records) follows the staged scene in dynamic LDS.
-    // Record r: 8-B words {ox, oy, oz, dx, dy, dz, rng} at
-    // s_poold[j * nslots + r], then 4-B words {k, q, su, hint, qv flags, q0x,
-    // q0y, q0z, q1x, q1y, q1z} at s_poolw[j * nslots + r]:
-    // each value moves with one LDS access straight from / into its register
-    constexpr unsigned nslots = kMigSlots;  // immediate offsets: one address register
-    double* s_poold = nullptr;
-    unsigned* s_poolw = nullptr;
-    auto mig_view = [&]() {
-      s_poold = (double*)(s_dyn + mig_read(&s_mig.off));
-      s_poolw = (unsigned*)(s_poold + 8 * nslots);
-    };
-    // One exchange per iteration of a drained wave (its queue empty, its
-    // refill block run), all under the workgroup's lock: idle lanes pop
-    // records (take); else a wave with 1..below live paths pushes them all
-    // and leaves (give), if another wave is still in the loop and the pool
-    // has room; a wave with no path and nothing to take leaves.
-    if (kMigC && exhausted && run_block && mig_read(&s_mig.slots) != 0) {
-      const uint64_t live_mask = __ballot(active);
-      const int live = (int)__popcll(live_mask);
-      const bool between = __ballot(active && (pending || sc_wait)) != 0;
-      if ((live < 64 && mig_read(&s_mig.count) > 0) || live <= mig_read(&s_mig.below)) {
-        mig_view();
-        mig_lock(&s_mig, lane);
-        const int cnt = mig_read(&s_mig.count);
-        const int n = min(cnt, 64 - live);
-        // a path moves between two bounces: not parked for a walk (pending)
-        // nor holding a resolved hit (sc_wait), so its state is the ray, its
-        // bounce count, stream and look-ahead queue (hit_quick forms the rest)
-        const bool give = n == 0 && live > 0 && !between && mig_read(&s_mig.alive) >= 2 &&
-                          cnt + live <= (int)nslots;
-        const bool leave = n == 0 && live == 0;
-        if (give && active) {
-          const unsigned sl = (unsigned)cnt + mbcnt64(live_mask);
-          s_poold[sl] = ox, s_poold[nslots + sl] = oy, s_poold[2 * nslots + sl] = oz;
-          s_poold[3 * nslots + sl] = dx, s_poold[4 * nslots + sl] = dy;
-          s_poold[5 * nslots + sl] = dz;
-          s_poold[6 * nslots + sl] = __builtin_bit_cast(double, rng);
-          s_poolw[sl] = (unsigned)k, s_poolw[nslots + sl] = q, s_poolw[2 * nslots + sl] = su;
-          s_poolw[3 * nslots + sl] = (unsigned)hint;
-          s_poolw[4 * nslots + sl] = (qv0 ? 1u : 0u) | (qv1 ? 2u : 0u);
-          s_poolw[5 * nslots + sl] = q0x, s_poolw[6 * nslots + sl] = q0y;
-          s_poolw[7 * nslots + sl] = q0z, s_poolw[8 * nslots + sl] = q1x;
-          s_poolw[9 * nslots + sl] = q1y, s_poolw[10 * nslots + sl] = q1z;
-        }
-        const unsigned r = mbcnt64(~live_mask);
-        if (!active && (int)r < n) {
-          const unsigned sl = (unsigned)(cnt - n) + r;
-          ox = s_poold[sl], oy = s_poold[nslots + sl], oz = s_poold[2 * nslots + sl];
-          dx = s_poold[3 * nslots + sl], dy = s_poold[4 * nslots + sl];
-          dz = s_poold[5 * nslots + sl];
-          rng = __builtin_bit_cast(uint64_t, s_poold[6 * nslots + sl]);
-          A = (dx * dx + dy * dy) + dz * dz;  // the same expression as where it was formed
-          k = (int)s_poolw[sl], q = s_poolw[nslots + sl], su = s_poolw[2 * nslots + sl];
-          hint = (int)s_poolw[3 * nslots + sl];
-          const unsigned fl = s_poolw[4 * nslots + sl];
-          qv0 = (fl & 1u) != 0, qv1 = (fl & 2u) != 0;
-          q0x = s_poolw[5 * nslots + sl], q0y = s_poolw[6 * nslots + sl];
-          q0z = s_poolw[7 * nslots + sl], q1x = s_poolw[8 * nslots + sl];
-          q1y = s_poolw[9 * nslots + sl], q1z = s_poolw[10 * nslots + sl];
-          active = true;  // (an idle lane is neither parked nor waiting: pending, sc_wait false)
-        }
-        if (lane == 0) {
-          s_mig.count = cnt - n + (give ? live : 0);
-          if (give || leave) s_mig.alive -= 1;
-        }
-        mig_unlock(&s_mig, lane);
-        if (give) active = false;
-      }
-    }
     clk.mark(kSecRefill);
-    // (a wave that gave its paths away, or found none to take, leaves here)
-    if (__ballot(active) == 0) return 1;
+    if (__ballot(active) == 0) break;
     if constexpr (kStamps) ++iters;
 
     // ---- world.hit(r, 0, inf, rec)  (main.cc:40) ----
@@ -1273,24 +1148,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
       active = false;
     }
     clk.mark(kSecFillShade);
-    // the queue is empty: the drain runs in the loop copy with the exchange
-    // (mig_slots != 0 only when the pool fits)
-    if constexpr (!kMigC && PSRT_MIG_SPLIT) {
-      if (exhausted && mig_read(&s_mig.slots) != 0) return 2;
-    }
-    return 0;
-  };
-#if PSRT_MIG_SPLIT  // A/B: the exchange only in a second copy of the loop
-  int st;
-  while ((st = step(std::false_type{})) == 0) {
   }
-  if (st == 2)
-    while (step(std::true_type{}) == 0) {
-    }
-#else
-  while (step(std::true_type{}) == 0) {
-  }
-#endif
   if constexpr (kStamps) {
     if (wlog) {
       const unsigned long long t = __builtin_amdgcn_s_memrealtime();
