@@ -14,6 +14,8 @@
 #pragma once
 
 #include <algorithm>
+#include <memory>
+#include <new>
 #include <cstdint>
 #include <ostream>
 #include <stdexcept>
@@ -25,12 +27,44 @@
 
 namespace psrt {
 
-struct frame {
-  int width = 0, height = 0, rows = 0, spp = 0;
-  std::vector<double> accum;        // rows x width x 3, reference order (top row first)
-  std::vector<unsigned char> rgb8;  // write_color bytes
-  rt_stats stats{};
+// Page-locked host memory (rt_host_alloc, include/rt.h) as a std allocator:
+// a frame held in it is written by the device directly, with no copy
+// (DESIGN.md §7 "Host buffers"). Pinning is slow: keep such a frame and
+// render into it again (render_into).
+template <class T>
+struct pinned_allocator {
+  using value_type = T;
+  pinned_allocator() = default;
+  template <class U>
+  pinned_allocator(const pinned_allocator<U>&) noexcept {}
+  T* allocate(size_t n) {
+    void* p = nullptr;
+    if (rt_host_alloc(n * sizeof(T), &p) != RT_OK || (!p && n)) throw std::bad_alloc();
+    return static_cast<T*>(p);
+  }
+  void deallocate(T* p, size_t) noexcept { rt_host_free(p); }
+  template <class U>
+  bool operator==(const pinned_allocator<U>&) const noexcept { return true; }
+  template <class U>
+  bool operator!=(const pinned_allocator<U>&) const noexcept { return false; }
 };
+
+template <template <class> class Alloc>
+struct basic_frame {
+  int width = 0, height = 0, rows = 0, spp = 0;
+  std::vector<double, Alloc<double>> accum;        // rows x width x 3, reference order (top row first)
+  std::vector<unsigned char, Alloc<unsigned char>> rgb8;  // write_color bytes
+  rt_stats stats{};
+  // sizes the buffers for a shard (no reallocation when they already fit)
+  void shape(int w, int h, int samples, int row_offset, int row_stride) {
+    width = w, height = h, spp = samples;
+    rows = std::max(0, rt_rows_owned(h, row_offset, row_stride));  // a shard may own none
+    accum.resize((size_t)rows * w * 3);
+    rgb8.resize((size_t)rows * w * 3);
+  }
+};
+using frame = basic_frame<std::allocator>;          // ordinary (pageable) memory
+using pinned_frame = basic_frame<pinned_allocator>;  // page-locked: no device-to-host copy
 
 inline void flatten_into(const hittable_list& list, std::vector<rt_sphere>& out) {
   for (const auto& obj : list.objects) {
@@ -75,10 +109,12 @@ inline void check_abi() {
                              std::to_string(RT_ABI_VERSION));
 }
 
-// main.cc:72-88 for output rows row_offset, row_offset+row_stride, ...
-inline frame render(const hittable_list& world, const camera& cam, int width, int height,
-                    int spp, int max_depth, uint64_t seed = 0, int row_offset = 0,
-                    int row_stride = 1) {
+// main.cc:72-88 for output rows row_offset, row_offset+row_stride, ...,
+// into f (a pinned_frame kept across frames takes the frame with no copy)
+template <class F>
+inline void render_into(F& f, const hittable_list& world, const camera& cam, int width, int height,
+                        int spp, int max_depth, uint64_t seed = 0, int row_offset = 0,
+                        int row_stride = 1) {
   check_abi();
   const std::vector<rt_sphere> spheres = flatten(world);
   const rt_camera c = to_rt(cam);
@@ -90,17 +126,17 @@ inline frame render(const hittable_list& world, const camera& cam, int width, in
   p.seed = seed;
   p.row_offset = row_offset;
   p.row_stride = row_stride;
-  frame f;
-  f.width = width;
-  f.height = height;
-  f.spp = spp;
-  f.rows = rt_rows_owned(height, row_offset, row_stride);
-  if (f.rows < 0) f.rows = 0;  // a shard that owns no rows renders nothing
-  f.accum.resize((size_t)f.rows * width * 3);
-  f.rgb8.resize((size_t)f.rows * width * 3);
+  f.shape(width, height, spp, row_offset, row_stride);
   check(rt_render(spheres.data(), (int)spheres.size(), &c, &p, f.accum.data(), f.rgb8.data(),
                   &f.stats),
         "rt_render");
+}
+
+inline frame render(const hittable_list& world, const camera& cam, int width, int height,
+                    int spp, int max_depth, uint64_t seed = 0, int row_offset = 0,
+                    int row_stride = 1) {
+  frame f;
+  render_into(f, world, cam, width, height, spp, max_depth, seed, row_offset, row_stride);
   return f;
 }
 
@@ -128,8 +164,9 @@ class device_group {
   void set_scene(const hittable_list& world, const camera& cam) {
     set_scene(flatten(world), to_rt(cam));
   }
-  frame render(int width, int height, int spp, int max_depth, uint64_t seed = 0,
-               int row_offset = 0, int row_stride = 1, unsigned flags = 0) {
+  template <class F>
+  void render_into(F& f, int width, int height, int spp, int max_depth, uint64_t seed = 0,
+                   int row_offset = 0, int row_stride = 1, unsigned flags = 0) {
     rt_params p{};
     p.width = width;
     p.height = height;
@@ -139,14 +176,13 @@ class device_group {
     p.row_offset = row_offset;
     p.row_stride = row_stride;
     p.flags = flags;
-    frame f;
-    f.width = width;
-    f.height = height;
-    f.spp = spp;
-    f.rows = std::max(0, rt_rows_owned(height, row_offset, row_stride));
-    f.accum.resize((size_t)f.rows * width * 3);
-    f.rgb8.resize((size_t)f.rows * width * 3);
+    f.shape(width, height, spp, row_offset, row_stride);
     check(rt_group_render(g_, &p, f.accum.data(), f.rgb8.data(), &f.stats), "rt_group_render");
+  }
+  frame render(int width, int height, int spp, int max_depth, uint64_t seed = 0,
+               int row_offset = 0, int row_stride = 1, unsigned flags = 0) {
+    frame f;
+    render_into(f, width, height, spp, max_depth, seed, row_offset, row_stride, flags);
     return f;
   }
 
@@ -182,13 +218,7 @@ inline frame render_materials(const std::vector<rt_sphere>& spheres,
   p.row_stride = row_stride;
   p.flags = RT_FLAG_MATERIALS;
   frame f;
-  f.width = width;
-  f.height = height;
-  f.spp = spp;
-  f.rows = rt_rows_owned(height, row_offset, row_stride);
-  if (f.rows < 0) f.rows = 0;
-  f.accum.resize((size_t)f.rows * width * 3);
-  f.rgb8.resize((size_t)f.rows * width * 3);
+  f.shape(width, height, spp, row_offset, row_stride);
   check(rt_render_materials(spheres.data(), mats.data(), (int)spheres.size(), &cam, &p,
                             f.accum.data(), f.rgb8.data(), &f.stats),
         "rt_render_materials");
@@ -246,14 +276,16 @@ inline camera to_camera(const rt_camera& c) {
 }
 
 // "P3\n<w> <rows>\n255\n" then one "r g b" line per pixel (main.cc:70, color.h:21-23)
-inline void write_ppm(std::ostream& out, const frame& f) {
+template <class F>
+inline void write_ppm(std::ostream& out, const F& f) {
   out << "P3\n" << f.width << ' ' << f.rows << "\n255\n";
   for (size_t k = 0; k < f.rgb8.size(); k += 3)
     out << (int)f.rgb8[k] << ' ' << (int)f.rgb8[k + 1] << ' ' << (int)f.rgb8[k + 2] << '\n';
 }
 
 // P6 (binary) variant of the same image
-inline void write_ppm_binary(std::ostream& out, const frame& f) {
+template <class F>
+inline void write_ppm_binary(std::ostream& out, const F& f) {
   out << "P6\n" << f.width << ' ' << f.rows << "\n255\n";
   out.write(reinterpret_cast<const char*>(f.rgb8.data()), (std::streamsize)f.rgb8.size());
 }

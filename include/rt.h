@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 /* ---- error codes ---------------------------------------------------------- */
 #define RT_OK 0
@@ -137,6 +137,15 @@ int rt_rows_owned(int height, int row_offset, int row_stride);
 int rt_render(const rt_sphere* spheres, int n_spheres, const rt_camera* cam,
               const rt_params* params, double* accum_rgb, unsigned char* rgb8,
               rt_stats* stats);
+
+/* Page-locked host memory for frame outputs (ABI 6). rt_render,
+ * rt_render_materials and rt_group_render recognise it: psrt_reduce then
+ * writes the sums and bytes straight into it across the link, with no
+ * device-to-host copy and no pageable staging (DESIGN.md §7 "Host buffers").
+ * Pinning is slow: allocate once and reuse across frames. Portable: usable
+ * by every device. RT_E_NOMEM if the pages cannot be locked. */
+int rt_host_alloc(size_t bytes, void** out);
+int rt_host_free(void* p);
 
 /* write_color (color.h:8-24) on host data: (int)(255.999*clamp(sqrt(c*(1/spp)),0,0.999)). */
 int rt_quantize_ppm(const double* accum_rgb, int width, int rows, int spp,

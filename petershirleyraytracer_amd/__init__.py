@@ -7,7 +7,7 @@ one-shot and device-resident renders, PPM output, and the multi-GPU sharding
 used by ``bench.py``. See DESIGN.md.
 """
 from .render import (Context, DeviceGroup, LensCamera, SceneFile, camera_default, camera_look_at,
-                     camera_look_at_lens, device_count, format_scene, load_scene, params,
+                     camera_look_at_lens, device_count, format_scene, host_array, load_scene, params,
                      parse_scene, ppm_p3, probe_f64, quantize, render, render_devices,
                      render_materials,
                      rows_owned, save_scene, scene_book_final, scene_random_spheres,
@@ -15,7 +15,7 @@ from .render import (Context, DeviceGroup, LensCamera, SceneFile, camera_default
 
 __all__ = [
     "Context", "DeviceGroup", "LensCamera", "SceneFile", "camera_default", "camera_look_at",
-    "camera_look_at_lens", "device_count", "format_scene", "load_scene", "params", "parse_scene",
+    "camera_look_at_lens", "device_count", "format_scene", "host_array", "load_scene", "params", "parse_scene",
     "ppm_p3", "probe_f64", "quantize", "render", "render_devices", "render_materials", "rows_owned", "save_scene",
     "scene_book_final", "scene_random_spheres", "scene_two_spheres", "get_tuning", "set_tuning",
     "tuning", "write_ppm",

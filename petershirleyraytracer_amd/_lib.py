@@ -12,9 +12,10 @@ from .build import LIB
 
 RT_OK = 0
 # include/rt.h RT_ABI_VERSION: the struct layouts below (RtStats grew in ABI 5)
+# and the entry points (rt_host_alloc / rt_host_free arrived in ABI 6)
 # are that version's, so a library of another version is refused at load
 # (tests/test_abi.py checks this constant against the header)
-ABI_VERSION = 5
+ABI_VERSION = 6
 ERRORS = {-1: "RT_E_INVALID", -2: "RT_E_HIP", -3: "RT_E_NODEVICE", -4: "RT_E_NOMEM",
           -5: "RT_E_SCENE"}
 
@@ -29,7 +30,7 @@ EXPORTS = [
     "rt_camera_look_at_lens", "rt_scene_book_final", "rt_context_set_materials",
     "rt_render_materials", "rt_context_set_tuning", "rt_context_get_tuning",
     "rt_group_create", "rt_group_destroy", "rt_group_size", "rt_group_context",
-    "rt_group_set_scene", "rt_group_render", "rt_render_devices",
+    "rt_group_set_scene", "rt_group_render", "rt_render_devices", "rt_host_alloc", "rt_host_free",
 ]
 
 
@@ -152,6 +153,8 @@ def load(build_if_missing: bool = False):
                             C.c_int),
         "rt_render_devices": ([P(RtSphere), C.c_int, P(RtCamera), P(RtParams), P(C.c_int),
                                C.c_int, P(C.c_double), P(C.c_ubyte), P(RtStats)], C.c_int),
+        "rt_host_alloc": ([C.c_size_t, P(C.c_void_p)], C.c_int),
+        "rt_host_free": ([C.c_void_p], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

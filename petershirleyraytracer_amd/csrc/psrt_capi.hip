@@ -1342,6 +1342,52 @@ int rt_quantize_device(rt_context* c, const double* d_accum, int width, int rows
   return RT_OK;
 }
 
+// The device address of page-locked host memory at p (rt_host_alloc,
+// hipHostMalloc, hipHostRegister), or nullptr for pageable memory: the
+// render's last kernels then write the caller's frame directly.
+static void* mapped_host(const void* p) {
+  if (!p) return nullptr;
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory: not an error of the render
+    return nullptr;
+  }
+  return at.type == hipMemoryTypeHost ? at.devicePointer : nullptr;
+}
+
+// One render of a one-shot entry into the caller's host buffers. Page-locked
+// buffers (rt_host_alloc) are the render's own outputs: psrt_reduce writes
+// the sums and bytes across the link as it forms them. Pageable ones receive
+// the device frame by copy (HIP stages it through its own pinned buffers).
+static int render_to_host(rt_context* c, const rt_params* p, double* accum_rgb,
+                          unsigned char* rgb8, rt_stats* stats) {
+  const int rows = rt_rows_owned(p->height, p->row_offset, p->row_stride);
+  const size_t P = rows > 0 ? (size_t)rows * p->width : 0;
+  double* h_acc = (double*)mapped_host(accum_rgb);
+  unsigned char* h_rgb = (unsigned char*)mapped_host(rgb8);
+  double* d_acc = h_acc;
+  unsigned char* d_rgb = h_rgb;
+  if ((accum_rgb && !h_acc) || (rgb8 && !h_rgb) || !accum_rgb) {
+    // the device frame (the running sums live on the device whenever the
+    // caller's are not device-visible or not wanted)
+    int rc = ensure_buf(c, &c->d_accum_tmp, &c->accum_tmp_cap, P * 3 + (P * 3 + 7) / 8 + 1);
+    if (rc) return rc;
+    if (!h_acc) d_acc = c->d_accum_tmp;
+    if (!h_rgb) d_rgb = (unsigned char*)(c->d_accum_tmp + P * 3);
+  }
+  int rc = rt_render_device(c, p, d_acc, rgb8 ? d_rgb : nullptr, nullptr);
+  if (rc) return rc;
+  if (accum_rgb && P && !h_acc)
+    HIP_TRY(hipMemcpyAsync(accum_rgb, d_acc, P * 3 * sizeof(double), hipMemcpyDeviceToHost,
+                           c->stream));
+  if (rgb8 && P && !h_rgb)
+    HIP_TRY(hipMemcpyAsync(rgb8, d_rgb, P * 3, hipMemcpyDeviceToHost, c->stream));
+  rc = rt_context_sync_stats(c, stats);  // waits for the render (and its copies)
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return RT_OK;
+}
+
 // The default context of RT_DEVICE, returned with that device's lock held
 // in *lock: the one-shot entries run whole under it, so host threads calling
 // them on one device take turns instead of sharing buffers mid-call.
@@ -1356,6 +1402,25 @@ static int get_default_context(rt_context** out, std::unique_lock<std::mutex>* l
   }
   *out = g_default[dev];
   (*out)->tune = tuning_defaults();  // the process defaults at each one-shot call
+  return RT_OK;
+}
+
+int rt_host_alloc(size_t bytes, void** out) {
+  if (!out) return set_error(RT_E_INVALID, "rt_host_alloc: out is NULL");
+  *out = nullptr;
+  if (bytes == 0) return RT_OK;
+  const hipError_t e = hipHostMalloc(out, bytes, hipHostMallocPortable | hipHostMallocMapped);
+  if (e != hipSuccess) {
+    *out = nullptr;
+    return set_error(e == hipErrorOutOfMemory ? RT_E_NOMEM : RT_E_HIP,
+                     "rt_host_alloc(%zu): %s", bytes, hipGetErrorString(e));
+  }
+  return RT_OK;
+}
+
+int rt_host_free(void* p) {
+  if (!p) return RT_OK;
+  HIP_TRY(hipHostFree(p));
   return RT_OK;
 }
 
@@ -1374,20 +1439,7 @@ int rt_render(const rt_sphere* sph, int n, const rt_camera* cam, const rt_params
   if (rc) return rc;
   rc = rt_context_set_scene(c, sph, n, cam);
   if (rc) return rc;
-  const int rows = rt_rows_owned(p->height, p->row_offset, p->row_stride);
-  const size_t P = (size_t)rows * p->width;
-  rc = ensure_buf(c, &c->d_accum_tmp, &c->accum_tmp_cap, P * 3 + (P * 3 + 7) / 8 + 1);
-  if (rc) return rc;
-  double* d_acc = c->d_accum_tmp;
-  unsigned char* d_rgb = (unsigned char*)(c->d_accum_tmp + P * 3);
-  rc = rt_render_device(c, p, d_acc, rgb8 ? d_rgb : nullptr, nullptr);
-  if (rc) return rc;
-  rc = rt_context_sync_stats(c, stats);
-  if (rc) return rc;
-  if (accum_rgb && P)
-    HIP_TRY(hipMemcpy(accum_rgb, d_acc, P * 3 * sizeof(double), hipMemcpyDeviceToHost));
-  if (rgb8 && P) HIP_TRY(hipMemcpy(rgb8, d_rgb, P * 3, hipMemcpyDeviceToHost));
-  return RT_OK;
+  return render_to_host(c, p, accum_rgb, rgb8, stats);
 }
 
 int rt_context_set_materials(rt_context* c, const rt_material* mats, int n,
@@ -1455,20 +1507,7 @@ int rt_render_materials(const rt_sphere* sph, const rt_material* mats, int n,
   if (rc) return rc;
   rc = rt_context_set_materials(c, mats, n, cam);
   if (rc) return rc;
-  const int rows = rt_rows_owned(q.height, q.row_offset, q.row_stride);
-  const size_t P = (size_t)rows * q.width;
-  rc = ensure_buf(c, &c->d_accum_tmp, &c->accum_tmp_cap, P * 3 + (P * 3 + 7) / 8 + 1);
-  if (rc) return rc;
-  double* d_acc = c->d_accum_tmp;
-  unsigned char* d_rgb = (unsigned char*)(c->d_accum_tmp + P * 3);
-  rc = rt_render_device(c, &q, d_acc, rgb8 ? d_rgb : nullptr, nullptr);
-  if (rc) return rc;
-  rc = rt_context_sync_stats(c, stats);
-  if (rc) return rc;
-  if (accum_rgb && P)
-    HIP_TRY(hipMemcpy(accum_rgb, d_acc, P * 3 * sizeof(double), hipMemcpyDeviceToHost));
-  if (rgb8 && P) HIP_TRY(hipMemcpy(rgb8, d_rgb, P * 3, hipMemcpyDeviceToHost));
-  return RT_OK;
+  return render_to_host(c, &q, accum_rgb, rgb8, stats);
 }
 
 // Debug entry: run one f64 primitive on the device (numerics parity tests).

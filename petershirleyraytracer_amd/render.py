@@ -19,6 +19,7 @@ cameras are ``(4, 3)`` float64 arrays (origin, lower_left, horizontal, vertical)
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 from contextlib import contextmanager
 from dataclasses import dataclass
 from typing import Optional
@@ -218,15 +219,50 @@ def stats_dict(s: RtStats) -> dict:
                 prerejects=s.prerejects, root_box_tests=s.root_box_tests)
 
 
+def host_array(shape, dtype=np.float64) -> np.ndarray:
+    """A numpy array in page-locked host memory (rt_host_alloc, include/rt.h):
+    passed as a render's output (render(..., out=...)), the frame is written
+    into it by the device across the link with no copy. Pinning is slow:
+    allocate once, reuse across frames. Freed with the array."""
+    L = _lib.load()
+    dt = np.dtype(dtype)
+    count = int(np.prod(shape)) if len(tuple(np.atleast_1d(shape))) else 1
+    nbytes = max(1, count * dt.itemsize)
+    ptr = C.c_void_p()
+    check(L.rt_host_alloc(nbytes, C.byref(ptr)), "rt_host_alloc")
+    buf = (C.c_ubyte * nbytes).from_address(ptr.value)
+    arr = np.frombuffer(buf, dtype=np.uint8, count=count * dt.itemsize).view(dt).reshape(shape)
+    weakref.finalize(buf, L.rt_host_free, C.c_void_p(ptr.value))
+    return arr
+
+
+def _out_arrays(out, rows: int, width: int, want_rgb: bool):
+    """The caller's output arrays (out = (accum, rgb8 or None)), checked, or new ones."""
+    if out is None:
+        return (np.zeros((rows, width, 3), dtype=np.float64),
+                np.zeros((rows, width, 3), dtype=np.uint8) if want_rgb else None)
+    acc, rgb = out
+    if acc.shape != (rows, width, 3) or acc.dtype != np.float64 or not acc.flags.c_contiguous:
+        raise ValueError(f"out accum must be C-contiguous float64 {(rows, width, 3)}")
+    if rgb is not None and (rgb.shape != (rows, width, 3) or rgb.dtype != np.uint8
+                            or not rgb.flags.c_contiguous):
+        raise ValueError(f"out rgb8 must be C-contiguous uint8 {(rows, width, 3)}")
+    if not acc.flags.writeable or (rgb is not None and not rgb.flags.writeable):
+        raise ValueError("out arrays must be writeable")
+    return acc, rgb
+
+
 def render(spheres, camera, width: int, height: int, spp: int, max_depth: int = 50,
            seed: int = 0, row_offset: int = 0, row_stride: int = 1, want_rgb: bool = True,
-           cull: bool = True, fixpoint: bool = True, cull_stats: bool = False):
+           cull: bool = True, fixpoint: bool = True, cull_stats: bool = False, out=None):
     """One-shot render of the owned rows on the default device (RT_DEVICE).
 
     cull=False forces the linear sweep; fixpoint=False traces provably trapped
     paths to max_depth. Neither changes a bit of the output.
     cull_stats=True counts the executed sphere / box tests (tests_executed,
     box_tests; 0 otherwise) with the slower counting kernel, same bits.
+    out=(accum, rgb8 or None): write into these arrays (e.g. host_array(...),
+    which the device writes directly) instead of new ones.
 
     Returns (accum[rows, W, 3] float64, rgb8[rows, W, 3] uint8 or None, stats dict).
     """
@@ -239,8 +275,7 @@ def render(spheres, camera, width: int, height: int, spp: int, max_depth: int = 
     # a shard that owns no rows (row_offset >= height: more ranks than rows)
     # renders nothing and returns empty [0, W, 3] blocks
     rows = max(0, L.rt_rows_owned(height, row_offset, row_stride))
-    acc = np.zeros((rows, width, 3), dtype=np.float64)
-    rgb = np.zeros((rows, width, 3), dtype=np.uint8) if want_rgb else None
+    acc, rgb = _out_arrays(out, rows, width, want_rgb)
     st = RtStats()
     check(L.rt_render(sp, n, C.byref(cam), C.byref(p),
                       acc.ctypes.data_as(C.POINTER(C.c_double)),
@@ -420,12 +455,13 @@ class DeviceGroup:
         check(self._L.rt_group_set_scene(self.handle, sp, n, C.byref(cam)), "rt_group_set_scene")
 
     def render(self, width: int, height: int, spp: int, max_depth: int = 50, seed: int = 0,
-               row_offset: int = 0, row_stride: int = 1, flags: int = 0, want_rgb: bool = True):
-        """Returns (accum[rows, W, 3], rgb8 or None, stats) of the shard."""
+               row_offset: int = 0, row_stride: int = 1, flags: int = 0, want_rgb: bool = True,
+               out=None):
+        """Returns (accum[rows, W, 3], rgb8 or None, stats) of the shard
+        (out=(accum, rgb8 or None): into these arrays, as render())."""
         p = params(width, height, spp, max_depth, seed, row_offset, row_stride, flags)
         rows = max(0, self._L.rt_rows_owned(height, row_offset, row_stride))
-        acc = np.zeros((rows, width, 3), dtype=np.float64)
-        rgb = np.zeros((rows, width, 3), dtype=np.uint8) if want_rgb else None
+        acc, rgb = _out_arrays(out, rows, width, want_rgb)
         st = RtStats()
         check(self._L.rt_group_render(self.handle, C.byref(p),
                                       acc.ctypes.data_as(C.POINTER(C.c_double)),

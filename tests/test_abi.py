@@ -38,7 +38,7 @@ def test_abi_version_and_info():
     L = _lib.load()
     hdr = open(os.path.join(ROOT, "include", "rt.h")).read()
     want = int(re.search(r"#define RT_ABI_VERSION (\d+)", hdr).group(1))
-    assert L.rt_abi_version() == want == _lib.ABI_VERSION == 5
+    assert L.rt_abi_version() == want == _lib.ABI_VERSION == 6
     assert b"gfx950" in L.rt_build_info()
 
 
@@ -199,3 +199,23 @@ def test_census_hooks_are_out_of_the_product_kernels():
         txt = open(os.path.join(csrc, f)).read()
         assert re.search(r"#if PSRT_(MAT_)?ABLATE ==", txt) is None, f
         assert "ablate_sink" not in txt, f
+
+
+def test_out_arrays_are_checked():
+    """render(out=...) rejects arrays of the wrong shape, type or layout before
+    any device work."""
+    sp, cam = P.scene_two_spheres(), P.camera_default()
+    with pytest.raises(ValueError, match="accum"):
+        P.render(sp, cam, 8, 4, 1, out=(np.zeros((4, 8, 2)), None))
+    with pytest.raises(ValueError, match="accum"):
+        P.render(sp, cam, 8, 4, 1, out=(np.zeros((4, 8, 3), np.float32), None))
+    with pytest.raises(ValueError, match="rgb8"):
+        P.render(sp, cam, 8, 4, 1, out=(np.zeros((4, 8, 3)), np.zeros((4, 8, 3))))
+    with pytest.raises(ValueError, match="accum"):
+        P.render(sp, cam, 8, 4, 1, out=(np.zeros((4, 8, 6))[:, :, ::2], None))
+
+
+@pytest.mark.skipif(have_gpu(), reason="checks the no-device path")
+def test_host_alloc_without_device_fails_loudly():
+    with pytest.raises(_lib.RtError):
+        P.host_array((4, 8, 3))

@@ -100,3 +100,15 @@ def test_host_app_rejects_bad_options(tmp_path):
         r = subprocess.run([exe, *bad, "-o", out, "--width", "8", "--height", "4", "--spp", "1"],
                            capture_output=True, text=True, timeout=60)
         assert r.returncode == 2, (bad, r.returncode, r.stderr)
+
+
+@pytest.mark.gpu
+def test_pinned_frames_bit_identical(tmp_path):
+    """psrt::pinned_frame (rt_host_alloc memory, written by the device with no
+    copy) holds the same bits as the ordinary frame through rt_render, a 1:3
+    shard and a three-member device group, and is reused without reallocation
+    (tests/host/pinned_frame.cc)."""
+    exe = str(tmp_path / "pinned")
+    _compile(os.path.join(ROOT, "tests", "host", "pinned_frame.cc"), exe)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", (r.stdout, r.stderr)
