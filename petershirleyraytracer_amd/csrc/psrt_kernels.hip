@@ -55,15 +55,6 @@ constexpr unsigned kWalkBatch = PSRT_WALK_BATCH;  // parked lanes that trigger a
 #define PSRT_WALK_TAIL 6  // r04 re-sweep (profiles/r04_knobs2): 2 / 4 / 6 / 8
 #endif
 constexpr unsigned kWalkTail = PSRT_WALK_TAIL;  // a BVH pass stops once this few lanes still walk
-#ifndef PSRT_RNG_GATE
-#define PSRT_RNG_GATE 0
-#endif
-#ifndef PSRT_RNG_G0
-#define PSRT_RNG_G0 1
-#endif
-#ifndef PSRT_RNG_G1
-#define PSRT_RNG_G1 1
-#endif
 #ifndef PSRT_RNG_FILL
 #define PSRT_RNG_FILL 2
 #endif
@@ -1107,15 +1098,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
       // branch-free body: every lane computes a trial; only lanes with room
       // take it (their stream advances), so the draws stay in stream order
       int f = 0;
-#if PSRT_RNG_GATE  // A/B: rounds 1 and 2 only while enough lanes have room
-      for (;;) {
-        const unsigned ng = (unsigned)__popcll(__ballot(can_fill && !qv1));
-        if (!((f < kRngFill && ng >= (f == 0 ? (unsigned)PSRT_RNG_G0 : (unsigned)PSRT_RNG_G1)) ||
-              (f < kRngFill + kRngExtra && __ballot(want && !qv0) != 0)))
-          break;
-#else
       do {
-#endif
         const bool go = can_fill && !qv1;
         if (go) clk.util(kUTrial);
         uint32_t z, y, x;
@@ -1130,13 +1113,9 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
         qv1 = qv1 || to1;
         qv0 = qv0 || to0;
         ++f;
-#if PSRT_RNG_GATE
-      }
-#else
       } while (f < kRngFill ||
                (f < kRngFill + kRngExtra &&
                 __ballot(want && !qv0) != 0));
-#endif
     }
     clk.mark(kSecFillShade);
 
