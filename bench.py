@@ -118,6 +118,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--save-ppm", default="")
     ap.add_argument("--no-cull", action="store_true", help="force the linear sphere sweep")
+    ap.add_argument("--assemble", default="auto", choices=("auto", "host", "gather"),
+                    help="N > 1: how the frame reaches host memory. host: every rank's reduce "
+                         "writes its interleaved rows into one page-locked shared-memory frame "
+                         "(one node); gather: RCCL gather of the rows to rank 0, then a copy to "
+                         "host; auto: host when all ranks share a node, else gather")
     ap.add_argument("--gather-fp64", action="store_true",
                     help="N > 1: gather the FP64 accumulators and quantise on rank 0 "
                          "(default: each rank quantises its rows, uint8 gather)")
@@ -381,7 +386,8 @@ def main():
     import torch.distributed as dist
 
     import petershirleyraytracer_amd as P
-    from petershirleyraytracer_amd.dist import gather_frame, gather_frames, rows_owned, shard
+    from petershirleyraytracer_amd.dist import (HostFrames, gather_frame, gather_frames,
+                                                rows_owned, shard)
     from petershirleyraytracer_amd.render import (FLAG_CULL_STATS, FLAG_NO_CULL, FLAG_NO_FIXPOINT,
                                                   FLAG_NO_TAIL_PRIORITY)
 
@@ -470,16 +476,35 @@ def main():
         scene_ms.append((time.perf_counter() - t0) * 1e3)
         ctxs.append(c)
     dev = torch.device("cuda", local)
+    # N > 1: how a step's frame reaches host memory (--assemble). "host": the
+    # ranks of one node share a page-locked frame (POSIX shared memory) and
+    # each rank's psrt_reduce writes its interleaved rows into it across its
+    # own GPU's link (rt_context_set_row_pitch): no collective, no copy on
+    # rank 0, eight links in parallel instead of rank 0's one. "gather": the
+    # RCCL gather over xGMI to rank 0, then rank 0 copies the frame to host.
+    assemble = "none"
+    if world > 1:
+        one_node = int(os.environ.get("LOCAL_WORLD_SIZE", world)) == world
+        assemble = args.assemble
+        if assemble == "auto":
+            assemble = "host" if one_node and not args.gather_fp64 else "gather"
+        if assemble == "host" and (not one_node or args.gather_fp64):
+            raise SystemExit("--assemble host needs every rank on one node and no --gather-fp64")
+    hostframes = None
+    if assemble == "host":
+        hostframes = HostFrames(depth * B, h, w, rank, world)
+        for c in ctxs:
+            c.set_row_pitch(0, world * w * 3)  # the sums stay packed on the device
     # per slot: B frames' accumulators and bytes
     acc = [torch.zeros((B, rows, w, 3), dtype=torch.float64, device=dev) for _ in range(depth)]
     rgb = torch.zeros((h, w, 3), dtype=torch.uint8, device=dev) if rank == 0 and world > 1 else None  # --gather-fp64
     rgb_rows = [torch.zeros((B, rows, w, 3), dtype=torch.uint8, device=dev)
-                for _ in range(depth)] if world > 1 else None
+                for _ in range(depth)] if assemble == "gather" else None
     # every step ends with the frame's bytes in pinned host memory (rank 0):
     # per slot and frame, so frames in flight never share one
     host_rows = h if world > 1 else rows
     host_rgb = [torch.empty((B, host_rows, w, 3), dtype=torch.uint8, pin_memory=True)
-                for _ in range(depth)] if rank == 0 else None
+                for _ in range(depth)] if rank == 0 and assemble != "host" else None
     # each frame slot renders on its context's own stream
     streams = [torch.cuda.ExternalStream(c.stream(), device=dev) for c in ctxs]
     # N > 1: every gather goes on one stream, in frame order on every rank
@@ -511,6 +536,14 @@ def main():
             # render and needs no copy of its own (which, as a kernel, would
             # wait for a CU slot behind the next frame's persistent launch)
             ctx.render_device_frames(run["prm"], nb, ptrs(acc[sl], nb), ptrs(host_rgb[sl], nb),
+                                     st.cuda_stream)
+            pending[sl] = (is_timed, None, nb)
+            return
+        if hostframes is not None:
+            # this rank's rows straight into the shared page-locked frames
+            # (slot sl owns frames sl*B .. sl*B + B - 1)
+            ctx.render_device_frames(run["prm"], nb, ptrs(acc[sl], nb),
+                                     [hostframes.rows_ptr(sl * B + f, w) for f in range(nb)],
                                      st.cuda_stream)
             pending[sl] = (is_timed, None, nb)
             return
@@ -735,6 +768,15 @@ def main():
     if world > 1:
         gathered = gather_frame(timed_first, h, rank, world)
         torch.cuda.synchronize(dev)
+    host_check = None
+    if hostframes is not None and rank == 0:
+        # frame 0 of every launch is seed --seed (the untimed launches after
+        # the timed region rewrite it with the same bits): the bytes the ranks
+        # wrote into host memory against write_color of the gathered FP64 frame
+        want = P.quantize(gathered.cpu().numpy(), spp)
+        got = hostframes.frames[last_sl * B]
+        host_check = {"frames_in_host_memory": depth * B, "assembled_by": world,
+                      "frame_equals_quantized_gathered_fp64": bool(np.array_equal(got, want))}
 
     if rank == 0:
         n = len(spheres)
@@ -778,7 +820,7 @@ def main():
                        "config_id": config_id, "width": w, **({"tune": args.tune} if args.tune else {}),
                        "height": h, "spp": spp, "max_depth": args.max_depth, "spheres": n,
                        "parallelism": (f"emulated shard {args.emulate_shard} (rows {off}::{stride})"
-                                       if args.emulate_shard else f"interleaved rows x{world}") + ((", RCCL FP64 framebuffer gather" if args.gather_fp64 else ", per-rank write_color + RCCL uint8 gather") if world > 1 else "")},
+                                       if args.emulate_shard else f"interleaved rows x{world}") + ((", RCCL FP64 framebuffer gather" if args.gather_fp64 else ", per-rank write_color into one shared page-locked host frame" if assemble == "host" else ", per-rank write_color + RCCL uint8 gather") if world > 1 else "")},
             "roofline": {
                 "bound": "valu",
                 "achieved": round(achieved / 1e12, 4),
@@ -827,9 +869,11 @@ def main():
             "unpipelined": unpiped,
             "per_rank": per_rank,
             "timed_step": ((f"{B} frames (seeds {args.seed}..{args.seed + B - 1}) per trace launch: " if B > 1 else "")
-                           + "render + write_color + " + ("RCCL uint8 gather + " if world > 1 and not args.gather_fp64 else "RCCL FP64 gather + psrt_quantize + " if world > 1 else "")
-                           + ("D2H of the frame's bytes into pinned host memory (rank 0)" if world > 1 else
+                           + "render + write_color + " + ("" if assemble in ("none", "host") else "RCCL uint8 gather + " if not args.gather_fp64 else "RCCL FP64 gather + psrt_quantize + ")
+                           + ("D2H: every rank's psrt_reduce writes its rows into one shared page-locked host frame" if assemble == "host" else
+                              "D2H of the frame's bytes into pinned host memory (rank 0)" if world > 1 else
                               "D2H: psrt_reduce writes the frame's bytes into pinned host memory")),
+            "frame_to_host": assemble,
             # one-time costs, outside the timed steps
             "one_time_ms": {"set_scene": round(scene_ms[0], 3),
                             "camera_lists": round(camlist_ms, 3),
@@ -840,6 +884,8 @@ def main():
         if args.save_ppm and rgb is not None:
             P.write_ppm(args.save_ppm, rgb.cpu().numpy(), binary=True)
         out["batch_check"] = batch_check
+        if host_check is not None:
+            out["host_frame_check"] = host_check
         cb, parity = None, None
         if world == 1 and not args.no_cpu_baseline:
             try:
@@ -873,6 +919,8 @@ def main():
     torch.cuda.synchronize(dev)
     for c in ctxs:
         c.close()
+    if hostframes is not None:
+        hostframes.close()
     if distributed:
         dist.destroy_process_group()
 

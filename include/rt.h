@@ -146,6 +146,11 @@ int rt_render(const rt_sphere* spheres, int n_spheres, const rt_camera* cam,
  * by every device. RT_E_NOMEM if the pages cannot be locked. */
 int rt_host_alloc(size_t bytes, void** out);
 int rt_host_free(void* p);
+/* Page-lock existing host memory (e.g. a frame in POSIX shared memory that
+ * several processes render into), with the same effect as rt_host_alloc
+ * memory; rt_host_unregister before the memory is freed or unmapped. */
+int rt_host_register(void* p, size_t bytes);
+int rt_host_unregister(void* p);
 
 /* write_color (color.h:8-24) on host data: (int)(255.999*clamp(sqrt(c*(1/spp)),0,0.999)). */
 int rt_quantize_ppm(const double* accum_rgb, int width, int rows, int spp,
@@ -161,6 +166,14 @@ int rt_context_destroy(rt_context* ctx);
 /* Flattened hittable_list + camera -> device constant buffers. */
 int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres,
                          int n_spheres, const rt_camera* cam);
+
+/* Output layout of the context's renders (ABI 6): consecutive rows of the
+ * shard land accum_pitch doubles / rgb8_pitch bytes apart (0 = packed,
+ * width * 3). With pitch G * width * 3 and the outputs pointing at row r of a
+ * full frame, the G shards r = 0..G-1 (row_offset r, row_stride G) assemble one
+ * frame in place: e.g. in page-locked host memory shared by G processes, with
+ * no gather. Not with RT_FLAG_MATERIALS. */
+int rt_context_set_row_pitch(rt_context* ctx, size_t accum_pitch, size_t rgb8_pitch);
 
 /* Enqueue a render of the owned rows on `stream` (after the context's
  * previous render, whatever its stream). A shard that owns no rows

@@ -31,6 +31,7 @@ EXPORTS = [
     "rt_render_materials", "rt_context_set_tuning", "rt_context_get_tuning",
     "rt_group_create", "rt_group_destroy", "rt_group_size", "rt_group_context",
     "rt_group_set_scene", "rt_group_render", "rt_render_devices", "rt_host_alloc", "rt_host_free",
+    "rt_host_register", "rt_host_unregister", "rt_context_set_row_pitch",
 ]
 
 
@@ -155,6 +156,9 @@ def load(build_if_missing: bool = False):
                                C.c_int, P(C.c_double), P(C.c_ubyte), P(RtStats)], C.c_int),
         "rt_host_alloc": ([C.c_size_t, P(C.c_void_p)], C.c_int),
         "rt_host_free": ([C.c_void_p], C.c_int),
+        "rt_host_register": ([C.c_void_p, C.c_size_t], C.c_int),
+        "rt_host_unregister": ([C.c_void_p], C.c_int),
+        "rt_context_set_row_pitch": ([C.c_void_p, C.c_size_t, C.c_size_t], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

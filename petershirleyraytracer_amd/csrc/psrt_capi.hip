@@ -236,6 +236,9 @@ struct rt_context {
   bool failed = false;    // the last render failed part-way (its timings are not reported)
   int fail_after = -1;    // rt_debug_fail_after_trace: the next render fails after this chunk
   psrt::Tuning tune;      // rt_context_set_tuning
+  // rt_context_set_row_pitch: rows of the outputs this far apart (0: packed)
+  size_t accum_pitch = 0;  // doubles
+  size_t rgb8_pitch = 0;   // bytes
   bool last_stamps = false;  // the last render ran the diagnostic variant (tune.stamps)
 };
 
@@ -692,6 +695,12 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
   if (!c) return set_error(RT_E_INVALID, "rt_render_device: ctx is NULL");
   int rc = check_params(p);
   if (rc) return rc;
+  if ((c->accum_pitch && c->accum_pitch < 3 * (size_t)p->width) ||
+      (c->rgb8_pitch && c->rgb8_pitch < 3 * (size_t)p->width))
+    return set_error(RT_E_INVALID, "row pitch (%zu doubles, %zu bytes) below 3 x width %d",
+                     c->accum_pitch, c->rgb8_pitch, p->width);
+  if ((c->accum_pitch || c->rgb8_pitch) && (p->flags & RT_FLAG_MATERIALS))
+    return set_error(RT_E_INVALID, "row pitches are not supported with RT_FLAG_MATERIALS");
   if (nframes < 1 || nframes > psrt::kMaxFrames)
     return set_error(RT_E_INVALID, "rt_render_device_frames: nframes %d outside [1, %d]", nframes,
                      psrt::kMaxFrames);
@@ -1162,9 +1171,15 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     // one launch reduces the frames concurrently: only when no two frames'
     // buffers overlap (a stride of at least one frame); overlapping buffers
     // keep the per-frame launches, in frame order
+    // a frame's footprint: its rows, row pitches apart (rt_context_set_row_pitch)
+    const size_t W3 = 3 * (size_t)p->width;
+    const size_t apitch = c->accum_pitch ? c->accum_pitch : W3;
+    const size_t rpitch = c->rgb8_pitch ? c->rgb8_pitch : W3;
+    const size_t acc_span = rows > 0 ? (size_t)(rows - 1) * apitch + W3 : 0;
+    const size_t rgb_span = rows > 0 ? (size_t)(rows - 1) * rpitch + W3 : 0;
     const bool one = strided(acc.data(), acc_stride) && strided(rgb_now.data(), rgb_stride) &&
-                     (nf == 1 || ((acc_stride == 0 || acc_stride >= 3 * P) &&
-                                  (rgb_stride == 0 || rgb_stride >= 3 * P)));
+                     (nf == 1 || ((acc_stride == 0 || acc_stride >= acc_span) &&
+                                  (rgb_stride == 0 || rgb_stride >= rgb_span)));
     for (size_t f0 = 0; f0 < nf; f0 += one ? nf : 1) {
       psrt::ReduceArgs ra{};
       ra.samp_t = c->d_samples + f0 * fu;
@@ -1179,6 +1194,9 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
       ra.frame_units = fu;
       ra.accum_stride = acc_stride;
       ra.rgb8_stride = rgb_stride;
+      ra.accum_pitch = apitch == W3 ? 0 : apitch;
+      ra.rgb8_pitch = rpitch == W3 ? 0 : rpitch;
+      ra.width = (unsigned)p->width;
       ra.fold_stats = f0 == 0;
       ra.fast_k = p->max_depth <= 1000;
       ra.heads = c->d_counters + kHeads;
@@ -1402,6 +1420,34 @@ static int get_default_context(rt_context** out, std::unique_lock<std::mutex>* l
   }
   *out = g_default[dev];
   (*out)->tune = tuning_defaults();  // the process defaults at each one-shot call
+  return RT_OK;
+}
+
+int rt_context_set_row_pitch(rt_context* c, size_t accum_pitch, size_t rgb8_pitch) {
+  if (!c) return set_error(RT_E_INVALID, "rt_context_set_row_pitch: ctx is NULL");
+  HIP_TRY(hipSetDevice(c->device));
+  {  // renders already enqueued keep the layout they were enqueued with
+    const int rc = quiesce(c);
+    if (rc) return rc;
+  }
+  c->accum_pitch = accum_pitch;
+  c->rgb8_pitch = rgb8_pitch;
+  return RT_OK;
+}
+
+int rt_host_register(void* p, size_t bytes) {
+  if (!p || !bytes) return set_error(RT_E_INVALID, "rt_host_register: bad arguments");
+  const hipError_t e =
+      hipHostRegister(p, bytes, hipHostRegisterPortable | hipHostRegisterMapped);
+  if (e != hipSuccess)
+    return set_error(e == hipErrorOutOfMemory ? RT_E_NOMEM : RT_E_HIP, "rt_host_register(%zu): %s",
+                     bytes, hipGetErrorString(e));
+  return RT_OK;
+}
+
+int rt_host_unregister(void* p) {
+  if (!p) return RT_OK;
+  HIP_TRY(hipHostUnregister(p));
   return RT_OK;
 }
 

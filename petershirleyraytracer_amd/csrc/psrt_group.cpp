@@ -37,6 +37,18 @@ struct Member {
   size_t cap = 0;  // pixels the buffers hold
 };
 
+// The device address of page-locked host memory (rt_host_alloc /
+// rt_host_register), or nullptr for pageable memory.
+void* mapped_host(const void* p) {
+  if (!p) return nullptr;
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return at.type == hipMemoryTypeHost ? at.devicePointer : nullptr;
+}
+
 int hip_err(hipError_t e, const char* what) {
   return psrt::set_error(e == hipErrorOutOfMemory ? RT_E_NOMEM : RT_E_HIP, "%s: %s", what,
                          hipGetErrorString(e));
@@ -63,6 +75,21 @@ int member_render(Member& mb, int g, int G, const rt_params& p, double* accum,
   const size_t P = (size_t)rows * q.width;
   hipError_t e = hipSetDevice(mb.device);
   if (e != hipSuccess) return hip_err(e, "hipSetDevice");
+  const size_t W3 = (size_t)q.width * 3;
+  // Page-locked caller buffers (rt_host_alloc): the member's reduce writes its
+  // rows straight into their places, G rows apart (rt_context_set_row_pitch),
+  // with no device buffers and no copy
+  double* h_acc = (double*)mapped_host(accum);
+  unsigned char* h_rgb = (unsigned char*)mapped_host(rgb8);
+  if (accum && h_acc && (!rgb8 || h_rgb)) {
+    int rc = rt_context_set_row_pitch(mb.ctx, (size_t)G * W3, (size_t)G * W3);
+    if (rc) return rc;
+    rc = rt_render_device(mb.ctx, &q, h_acc + (size_t)g * W3, rgb8 ? h_rgb + (size_t)g * W3 : nullptr,
+                          nullptr);
+    if (!rc) rc = rt_context_sync_stats(mb.ctx, st);  // waits for the render
+    const int rc2 = rt_context_set_row_pitch(mb.ctx, 0, 0);
+    return rc ? rc : rc2;
+  }
   if (mb.cap < P) {
     (void)hipFree(mb.d_accum);
     (void)hipFree(mb.d_rgb);
@@ -84,7 +111,6 @@ int member_render(Member& mb, int g, int G, const rt_params& p, double* accum,
     return code;
   };
   // row k of this member is row g + kG of the caller's shard
-  const size_t W3 = (size_t)q.width * 3;
   if (accum &&
       (e = hipMemcpy2DAsync(accum + (size_t)g * W3, (size_t)G * W3 * sizeof(double), mb.d_accum,
                             W3 * sizeof(double), W3 * sizeof(double), (size_t)rows,

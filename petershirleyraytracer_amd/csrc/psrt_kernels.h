@@ -196,6 +196,12 @@ struct ReduceArgs {
   size_t frame_units;
   size_t accum_stride;  // doubles
   size_t rgb8_stride;   // bytes
+  // Row pitches of the outputs (rt_context_set_row_pitch), 0 = packed rows:
+  // pixel q = row * width + i of the shard at accum + row * accum_pitch + 3 i
+  // (doubles) and rgb8 + row * rgb8_pitch + 3 i (bytes), so G shards can write
+  // their interleaved rows straight into one frame
+  size_t accum_pitch, rgb8_pitch;
+  unsigned width;
   // Statistics and queue state of the trace launch before this reduce
   // (block 0 only): the counter sets are added into totals (reset on the first
   // chunk), then the sets and the queue heads are zeroed for the next launch;

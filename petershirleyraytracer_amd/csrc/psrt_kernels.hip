@@ -1228,10 +1228,15 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
   const unsigned q = q0 + lane;
   const unsigned S = (unsigned)a.s_count;
   double r = 0.0, g = 0.0, b = 0.0;
+  // this lane's sums (ReduceArgs::accum_pitch: rows may lie apart)
+  double* const acc_q =
+      !a.accum ? nullptr
+      : a.accum_pitch ? a.accum + (size_t)(q / a.width) * a.accum_pitch + (size_t)(q % a.width) * 3
+                      : a.accum + (size_t)q * 3;
   if (!a.first_chunk && q < a.pixels) {
-    r = a.accum[(size_t)q * 3 + 0];
-    g = a.accum[(size_t)q * 3 + 1];
-    b = a.accum[(size_t)q * 3 + 2];
+    r = acc_q[0];
+    g = acc_q[1];
+    b = acc_q[2];
   }
   // Tiles of a pixel run: kReduceTile doubles of t and kReduceTile uint16 of
   // k per pixel. With s_count % 4 == 0 they are 16-B aligned: t is read in
@@ -1345,9 +1350,9 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
     }
   }
   if (a.accum && q < a.pixels) {
-    a.accum[(size_t)q * 3 + 0] = r;
-    a.accum[(size_t)q * 3 + 1] = g;
-    a.accum[(size_t)q * 3 + 2] = b;
+    acc_q[0] = r;
+    acc_q[1] = g;
+    acc_q[2] = b;
   }
   if (a.rgb8) {  // write_color (color.h:8-24)
     __shared__ __attribute__((aligned(16))) unsigned char s_rgb[kReduceBlock * 3];
@@ -1364,12 +1369,23 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
     // The wave's pixels are 192 contiguous bytes: written as 12 x 16-B stores
     // (the frame may be pinned host memory, written across the link: the
     // frame's device-to-host transfer then needs no copy of its own)
-    unsigned char* const dst = a.rgb8 + (size_t)q0 * 3;
     const unsigned nb = min((unsigned)kReduceBlock, a.pixels - q0) * 3u;
-    if (nb == kReduceBlock * 3u && ((uintptr_t)dst & 15u) == 0) {
-      if (lane < kReduceBlock * 3 / 16) ((uint4*)dst)[lane] = ((const uint4*)s_rgb)[lane];
+    if (!a.rgb8_pitch) {
+      unsigned char* const dst = a.rgb8 + (size_t)q0 * 3;
+      if (nb == kReduceBlock * 3u && ((uintptr_t)dst & 15u) == 0) {
+        if (lane < kReduceBlock * 3 / 16) ((uint4*)dst)[lane] = ((const uint4*)s_rgb)[lane];
+      } else {
+        for (unsigned e = lane; e < nb; e += kReduceBlock) dst[e] = s_rgb[e];
+      }
     } else {
-      for (unsigned e = lane; e < nb; e += kReduceBlock) dst[e] = s_rgb[e];
+      // rows rgb8_pitch apart (another shard's rows between them): each byte
+      // to its row; a wave's bytes stay contiguous within a row, so the
+      // stores still coalesce
+      for (unsigned e = lane; e < nb; e += kReduceBlock) {
+        const unsigned qq = q0 + e / 3;
+        a.rgb8[(size_t)(qq / a.width) * a.rgb8_pitch + (size_t)(qq % a.width) * 3 + e % 3] =
+            s_rgb[e];
+      }
     }
   }
 }

@@ -3,15 +3,21 @@
 Rank g of G owns output rows r = g, g+G, g+2G, ... (rt_params.row_offset = g,
 row_stride = G). Every (pixel, sample) is independent under the counter RNG,
 so the shards need no exchange while rendering; the one exchange step is the
-framebuffer gather to rank 0 (RCCL over xGMI with backend "nccl", gloo on
-CPU). Interleaving balances the load: contiguous row bands of the final scene
+framebuffer's assembly on rank 0: on one node, in a page-locked frame in
+shared host memory that every rank writes its rows into (HostFrames), or by
+a gather to rank 0 (RCCL over xGMI with backend "nccl", gloo on CPU).
+Interleaving balances the load: contiguous row bands of the final scene
 cost 0.15-1.32x the mean. The gathered frame is bit-identical
 for any G because each pixel's accumulation never leaves its lane.
 """
 from __future__ import annotations
 
+import ctypes as C
+import uuid
+from multiprocessing import shared_memory
 from typing import Optional, Tuple
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -81,3 +87,65 @@ def _gather_blocks(local: torch.Tensor, height: int, rank: int, world: int,
         if n:
             frames[:, r::world] = parts[r][:, :n]
     return frames
+
+
+class HostFrames:
+    """Frames assembled in place in page-locked host memory shared by the
+    ranks of one node (DESIGN.md §5 "Frame to host"): rank 0 creates a POSIX
+    shared-memory segment of `nframes` frames [H, W, 3] uint8, every rank maps
+    it and page-locks it (rt_host_register), and each rank's psrt_reduce writes
+    its interleaved rows straight into it (rt_context_set_row_pitch: rows
+    G * W * 3 bytes apart). Every rank's bytes cross its own GPU's link, in
+    parallel; no collective and no device-to-host copy on rank 0. The frames
+    are complete on every rank once all ranks' renders are done (a barrier).
+    Collective: every rank constructs it; close() on every rank."""
+
+    def __init__(self, nframes: int, height: int, width: int, rank: int, world: int):
+        from . import _lib
+        self._L = _lib.load()
+        self.shape = (nframes, height, width, 3)
+        self.frame_bytes = height * width * 3
+        size = max(1, nframes * self.frame_bytes)
+        self.owner = rank == 0
+        self.shm = None
+        name = [None]
+        if self.owner:  # created before its name goes out
+            self.shm = shared_memory.SharedMemory(name=f"psrt_{uuid.uuid4().hex[:16]}",
+                                                  create=True, size=size)
+            name[0] = self.shm.name
+        try:
+            dist.broadcast_object_list(name, src=0)
+            if not self.owner:
+                self.shm = shared_memory.SharedMemory(name=name[0], create=False, size=size)
+                # the owner unlinks it below: the other ranks' resource trackers
+                # must not try again at exit (Python < 3.13 registers attaches too)
+                from multiprocessing import resource_tracker
+                try:
+                    resource_tracker.unregister(self.shm._name, "shared_memory")
+                except Exception:
+                    pass
+            dist.barrier()  # every rank has mapped it before the owner may unlink
+        finally:
+            if self.owner:
+                self.shm.unlink()  # the mappings stay; nothing is left in /dev/shm
+        self.frames = np.ndarray(self.shape, dtype=np.uint8, buffer=self.shm.buf)
+        self.addr = C.addressof(C.c_ubyte.from_buffer(self.shm.buf))
+        _lib.check(self._L.rt_host_register(C.c_void_p(self.addr), size), "rt_host_register")
+        self.registered = True
+        self.row_offset, self.row_stride = rank, world
+
+    def rows_ptr(self, f: int, width: int) -> int:
+        """Frame f's first row of this rank's shard."""
+        return self.addr + f * self.frame_bytes + self.row_offset * width * 3
+
+    def close(self) -> None:
+        if getattr(self, "registered", False):
+            self._L.rt_host_unregister(C.c_void_p(self.addr))
+            self.registered = False
+        if getattr(self, "shm", None) is not None:
+            self.frames = None
+            try:
+                self.shm.close()
+            except BufferError:
+                pass
+            self.shm = None

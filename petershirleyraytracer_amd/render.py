@@ -403,6 +403,12 @@ class Context:
         chunk `chunk`'s trace launch, before its reduce (rt_debug_fail_after_trace)."""
         check(self._L.rt_debug_fail_after_trace(self.handle, chunk), "rt_debug_fail_after_trace")
 
+    def set_row_pitch(self, accum_pitch: int = 0, rgb8_pitch: int = 0) -> None:
+        """rt_context_set_row_pitch: the shard's output rows this many doubles /
+        bytes apart (0 = packed), so shards can write one frame in place."""
+        check(self._L.rt_context_set_row_pitch(self.handle, accum_pitch, rgb8_pitch),
+              "rt_context_set_row_pitch")
+
     def set_tuning(self, name: str, value: float) -> None:
         """rt_context_set_tuning on this context (measurement / test knobs)."""
         set_tuning(name, value, self)

@@ -81,6 +81,27 @@ def test_bench_two_ranks_gathered_frame_matches_reference():
     par = d["parity_vs_cpu"]
     assert par["checked"] is True, par
     assert par["fp64_bit_identical"] is True and par["ranks_covered"] == 2, par
+    # one node: the ranks assemble the frame in shared page-locked host memory
+    assert d["frame_to_host"] == "host", d["frame_to_host"]
+    assert d["host_frame_check"]["frame_equals_quantized_gathered_fp64"] is True, d["host_frame_check"]
+
+
+def test_bench_two_ranks_gather_path():
+    """--assemble gather: the rows gathered to rank 0 by the collective (RCCL
+    on the driver's node; gloo here), then copied to host on rank 0."""
+    _require_ref()
+    env = dict(os.environ, PSRT_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1",
+               OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+           "--gpus", "2", "--config", "c1", "--steps", "3", "--warmup", "1", "--pipeline", "1",
+           "--assemble", "gather"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["frame_to_host"] == "gather" and "host_frame_check" not in d
+    par = d["parity_vs_cpu"]
+    assert par["checked"] is True and par["fp64_bit_identical"] is True, par
 
 
 def test_bench_two_ranks_c4_gathered_frame_checked():
@@ -104,6 +125,7 @@ def test_bench_two_ranks_c4_gathered_frame_checked():
     assert par["checked"] is True, par
     assert par["fp64_bit_identical"] is True and par["ranks_covered"] == 2, par
     assert par["spp"] == 500, par
+    assert d["host_frame_check"]["frame_equals_quantized_gathered_fp64"] is True, d["host_frame_check"]
 
 
 def test_bench_eight_ranks_driver_command():
@@ -129,3 +151,6 @@ def test_bench_eight_ranks_driver_command():
     assert par["ranks_covered"] == 8, par
     bc = d["batch_check"]
     assert bc["all_ranks_equal"] is True and bc["last_frame_equal"] is True, bc
+    hc = d["host_frame_check"]
+    assert d["frame_to_host"] == "host" and hc["assembled_by"] == 8, hc
+    assert hc["frame_equals_quantized_gathered_fp64"] is True, hc

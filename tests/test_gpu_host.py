@@ -64,3 +64,32 @@ def test_group_into_pinned(final_scene, cam):
     g.render(96, 64, 8, seed=5, out=(acc, rgb))
     g.close()
     assert np.array_equal(bits(acc), bits(want)) and np.array_equal(rgb, wrgb)
+
+
+def test_row_pitch_shards_assemble_one_frame(final_scene, cam):
+    """rt_context_set_row_pitch: three contexts render the shards r::3 with
+    their rows 3 x W x 3 apart, straight into one frame (device memory for the
+    sums, page-locked host memory for the bytes): the frame equals a
+    one-context render bit for bit."""
+    import torch
+    want, wrgb, _ = P.render(final_scene, cam, 96, 64, 8, seed=7)
+    W3 = 96 * 3
+    acc = torch.zeros((64, 96, 3), dtype=torch.float64, device="cuda")
+    rgb = P.host_array((64, 96, 3), np.uint8)
+    ctxs = [P.Context(0) for _ in range(3)]
+    for r, c in enumerate(ctxs):
+        c.set_scene(final_scene, cam)
+        c.set_row_pitch(3 * W3, 3 * W3)
+        c.render_device(P.params(96, 64, 8, 50, 7, r, 3), acc.data_ptr() + r * W3 * 8,
+                        rgb.ctypes.data + r * W3)
+    for c in ctxs:
+        c.sync_stats()
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(acc.cpu().numpy()), bits(want)) and np.array_equal(rgb, wrgb)
+    # rows closer than one row apart are an error, so are pitches with materials
+    from petershirleyraytracer_amd import _lib
+    with pytest.raises(_lib.RtError, match="row pitch"):
+        ctxs[0].set_row_pitch(10, 0)
+        ctxs[0].render_device(P.params(96, 64, 8, 50, 7, 0, 3), acc.data_ptr(), 0)
+    for c in ctxs:
+        c.close()
