@@ -134,6 +134,11 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=0,
                     help="launches in flight (0 = auto: measured among 1..3 for one-frame "
                          "launches of single-chunk frames, else 1)")
+    ap.add_argument("--no-drain-gate", action="store_true",
+                    help="frames in flight: start the next launch at once instead of when the "
+                         "previous one's work queue empties (rt_context_wait_drain; A/B)")
+    ap.add_argument("--no-lean-reduce", action="store_true",
+                    help="frames in flight: keep psrt_reduce instead of psrt_reduce_lean (A/B)")
     ap.add_argument("--scaling", default="strong", choices=("weak", "strong"),
                     help="strong (default): the configured frame on any N; weak (study): "
                          "N GPUs render the frame at N x spp (per-GPU work fixed)")
@@ -515,7 +520,7 @@ def main():
             dist.barrier()
 
     pending = [None] * depth  # per slot: (timed?, event after the gathers, frames)
-    run = {"dn": depth, "kms": [], "rays": [], "exec": [], "frames": [], "prm": prm}
+    run = {"dn": depth, "kms": [], "rays": [], "exec": [], "frames": [], "prm": prm, "prev": None}
 
     def ptrs(t, nb):
         # frame f's block by address arithmetic: t[f].data_ptr() builds a view
@@ -527,6 +532,12 @@ def main():
         """Launch i of a timed() sequence: nb frames in one rt_render_device_frames."""
         sl = i % run["dn"]
         ctx, st = ctxs[sl], streams[sl]
+        # frames in flight: this launch starts when the previous one's queue
+        # is empty, in its tail (two persistent launches that share the GPU
+        # from their start lose more than the tail costs, DESIGN.md §7)
+        if run["dn"] > 1 and run["prev"] is not None and not args.no_drain_gate:
+            ctxs[run["prev"]].wait_drain(st.cuda_stream)
+        run["prev"] = sl
         if timeline and is_timed and "tl_call" not in run:
             run["tl_call"] = time.monotonic_ns()
         if world == 1:
@@ -610,7 +621,13 @@ def main():
         dn launches in flight; the timed frames start from an idle GPU and end
         when the last one is done."""
         b = b or B
-        run.update(dn=dn, kms=[], rays=[], exec=[], frames=[],
+        # frames in flight: each frame's reduce must fit beside the next
+        # frame's resident trace, or it waits for that trace's tail
+        # (psrt_reduce_lean, DESIGN.md §7); one launch at a time: psrt_reduce
+        lean = 1 if dn > 1 and not args.no_lean_reduce else 0
+        for c in ctxs:
+            c.set_tuning("reduce_lean", lean)
+        run.update(dn=dn, kms=[], rays=[], exec=[], frames=[], prev=None,
                    prm=prm_count if count else (prm if tail else prm_notail))
         seq = [(nb, False) for nb in batches(nwarm, b)] + [(nb, True) for nb in batches(nsteps, b)]
         t0 = None

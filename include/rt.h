@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 6
+#define RT_ABI_VERSION 7
 
 /* ---- error codes ---------------------------------------------------------- */
 #define RT_OK 0
@@ -174,6 +174,18 @@ int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres,
  * frame in place: e.g. in page-locked host memory shared by G processes, with
  * no gather. Not with RT_FLAG_MATERIALS. */
 int rt_context_set_row_pitch(rt_context* ctx, size_t accum_pitch, size_t rgb8_pitch);
+
+/* Frames in flight (ABI 7): enqueue on `stream` a wait until ctx's last
+ * enqueued trace launch has emptied its work queue (its first wave found no
+ * more work: the launch's tail begins). A render enqueued on `stream` next,
+ * with another context, then starts while ctx's last waves drain and takes
+ * the CU slots their workgroups release, instead of sharing the GPU with
+ * ctx's launch from its start or waiting for its end (bench.py frames in
+ * flight). The wait holds however late it is enqueued: the
+ * launch stores its number (counted per context, never reset) in a flag.
+ * No-op before ctx's first render; RT_E_HIP if the device offers no signal
+ * memory to wait on. */
+int rt_context_wait_drain(const rt_context* ctx, void* stream);
 
 /* Enqueue a render of the owned rows on `stream` (after the context's
  * previous render, whatever its stream). A shard that owns no rows
@@ -390,6 +402,8 @@ int rt_debug_world_hit_hint(const rt_sphere* spheres, int n_spheres, const doubl
  *   stamps          1: the diagnostic kernel variant (section clocks on stderr)
  *   scene_rebuild   1: rebuild the culling structures for an unchanged scene
  *   big_ratio       radius ratio of the big-sphere class (0: 16)
+ *   reduce_lean     1: psrt_reduce_lean, which fits beside a resident trace
+ *                   launch (frames in flight; max_depth <= 1000 only)
  * ctx == NULL sets / reads the process defaults: a context copies them at
  * rt_context_create, the one-shot entries' default contexts at every call.
  * Unknown names and non-finite values fail with RT_E_INVALID. */

@@ -12,10 +12,11 @@ from .build import LIB
 
 RT_OK = 0
 # include/rt.h RT_ABI_VERSION: the struct layouts below (RtStats grew in ABI 5)
-# and the entry points (rt_host_alloc / rt_host_free arrived in ABI 6)
+# and the entry points (rt_host_alloc / rt_host_free arrived in ABI 6,
+# rt_context_wait_drain in ABI 7)
 # are that version's, so a library of another version is refused at load
 # (tests/test_abi.py checks this constant against the header)
-ABI_VERSION = 6
+ABI_VERSION = 7
 ERRORS = {-1: "RT_E_INVALID", -2: "RT_E_HIP", -3: "RT_E_NODEVICE", -4: "RT_E_NOMEM",
           -5: "RT_E_SCENE"}
 
@@ -32,6 +33,7 @@ EXPORTS = [
     "rt_group_create", "rt_group_destroy", "rt_group_size", "rt_group_context",
     "rt_group_set_scene", "rt_group_render", "rt_render_devices", "rt_host_alloc", "rt_host_free",
     "rt_host_register", "rt_host_unregister", "rt_context_set_row_pitch",
+    "rt_context_wait_drain",
 ]
 
 
@@ -159,6 +161,7 @@ def load(build_if_missing: bool = False):
         "rt_host_register": ([C.c_void_p, C.c_size_t], C.c_int),
         "rt_host_unregister": ([C.c_void_p], C.c_int),
         "rt_context_set_row_pitch": ([C.c_void_p, C.c_size_t, C.c_size_t], C.c_int),
+        "rt_context_wait_drain": ([C.c_void_p, C.c_void_p], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -103,6 +103,7 @@ struct Tuning {
   double stamps = 0;         // diagnostic kernel variant (section clocks, utilisation probes)
   double scene_rebuild = 0;  // rebuild the culling structures for an unchanged scene
   double big_ratio = 0;      // radius ratio of the big-sphere class (0: psrt_bvh's default)
+  double reduce_lean = 0;    // psrt_reduce_lean (fits beside a resident trace: frames in flight)
 };
 }  // namespace psrt
 
@@ -132,6 +133,7 @@ const TuningKey kTuningKeys[] = {
     {"stamps", &psrt::Tuning::stamps, 0, 1},
     {"scene_rebuild", &psrt::Tuning::scene_rebuild, 0, 1},
     {"big_ratio", &psrt::Tuning::big_ratio, 0, 1e300},
+    {"reduce_lean", &psrt::Tuning::reduce_lean, 0, 1},
 };
 std::mutex g_tuning_mu;
 psrt::Tuning g_tuning;  // the process defaults (rt_context_set_tuning(NULL, ...))
@@ -240,6 +242,14 @@ struct rt_context {
   size_t accum_pitch = 0;  // doubles
   size_t rgb8_pitch = 0;   // bytes
   bool last_stamps = false;  // the last render ran the diagnostic variant (tune.stamps)
+  // Drain flag (rt_context_wait_drain): HSA signal memory that each trace
+  // launch's waves set to its epoch once its work queue is empty; epochs count
+  // the context's enqueued trace launches (never reset, so a late wait holds)
+  unsigned long long* d_drain = nullptr;
+  unsigned long long drain_epoch = 0;
+  // psrt_reduce_lean fits beside a resident trace only within 32 VGPRs (and
+  // 16 SGPRs: tests/test_abi.py reads the code object's counts)
+  bool lean_ok = false;
 };
 
 namespace {
@@ -369,6 +379,13 @@ int rt_context_create(int device, rt_context** out) {
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, psrt::psrt_trace_mat<true, false, false>,
                                                         psrt::kMatBlock, 0));
   c->grid_mat_bvh = c->cus * (per_cu < 1 ? 1 : per_cu);
+  {
+    hipFuncAttributes fa{};
+    HIP_TRY(hipFuncGetAttributes(&fa, (const void*)psrt::psrt_reduce_lean));
+    c->lean_ok = fa.numRegs <= 32 && fa.sharedSizeBytes == 0;
+    HIP_TRY(hipFuncGetAttributes(&fa, (const void*)psrt::psrt_fold_stats));
+    c->lean_ok = c->lean_ok && fa.numRegs <= 32 && fa.sharedSizeBytes == 0;
+  }
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIP_TRY(hipMalloc(&c->d_counters, kCounterWords * sizeof(unsigned long long)));
   // zeroed once: psrt_reduce leaves the queue heads and counter sets at zero
@@ -382,6 +399,15 @@ int rt_context_create(int device, rt_context** out) {
   HIP_TRY(hipEventCreate(&c->ev_all1));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_plist, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_mat_plist, hipEventDisableTiming));
+  // the drain flag (optional: without it rt_context_wait_drain reports RT_E_HIP)
+  if (hipExtMallocWithFlags((void**)&c->d_drain, sizeof(unsigned long long),
+                            hipMallocSignalMemory) != hipSuccess) {
+    (void)hipGetLastError();
+    c->d_drain = nullptr;
+  } else {
+    HIP_TRY(hipStreamWriteValue64(c->stream, c->d_drain, 0, 0));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  }
   *out = c;
   return RT_OK;
 }
@@ -400,6 +426,7 @@ int rt_context_destroy(rt_context* c) {
   (void)hipFree(c->d_mat_plist);
   (void)hipFree(c->d_wave_log);
   (void)hipFree(c->d_counters);
+  if (c->d_drain) (void)hipFree(c->d_drain);
   (void)hipFree(c->d_nodes);
   (void)hipFree(c->d_leaf_geo);
   (void)hipFree(c->d_leaf_idx);
@@ -915,6 +942,7 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
   ta.div_w = fast_div_make((unsigned)p->width);
   ta.work_counter = c->d_counters + kHeads;
   ta.ray_counter = c->d_counters + kSets;
+  ta.drain_flag = c->d_drain;
 
   // No memset here: the queue heads and counter sets are zero (context
   // creation, then every psrt_reduce), and a small fill kernel on this stream
@@ -1135,6 +1163,7 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     };
     using T = std::true_type;
     using F = std::false_type;
+    ta.drain_epoch = c->drain_epoch + 1;  // counted once the launch is enqueued
     if (!use_bvh)
       stamps ? pick(F{}, T{}, F{}, c->grid) : pick(F{}, F{}, F{}, c->grid);
     else if (lds)
@@ -1142,6 +1171,7 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
     else
       stamps ? pick(T{}, T{}, F{}, c->grid_bvh) : pick(T{}, F{}, F{}, c->grid_bvh);
     HIP_TRY(hipGetLastError());
+    c->drain_epoch = ta.drain_epoch;
     HIP_TRY(hipEventRecord(c->ev[2 * ch + 1], st));
     if (ch == fail_at)
       return set_error(RT_E_HIP, "rt_debug_fail_after_trace: failure injected after chunk %d", ch);
@@ -1204,8 +1234,14 @@ int rt_render_device_frames(rt_context* c, const rt_params* p, int nframes,
       ra.totals = c->d_counters + kTotals;
       ra.host_stats = (last && f0 == 0) ? c->d_stats : nullptr;
       const unsigned blocks = (unsigned)((P + psrt::kReduceBlock - 1) / psrt::kReduceBlock);
-      hipLaunchKernelGGL(psrt::psrt_reduce, dim3(blocks, one ? (unsigned)nf : 1u),
-                         dim3(psrt::kReduceBlock), 0, st, ra);
+      // Tuning::reduce_lean (frames in flight): the variant that fits beside a
+      // resident trace launch, when its register count allows (lean_ok)
+      const bool lean = c->tune.reduce_lean != 0 && ra.fast_k && sc % 4 == 0 && c->lean_ok;
+      ra.inv_spp = 1.0 / (double)p->spp;
+      if (lean && ra.fold_stats)  // the fold psrt_reduce_lean leaves out
+        hipLaunchKernelGGL(psrt::psrt_fold_stats, dim3(1), dim3(64), 0, st, ra);
+      hipLaunchKernelGGL(lean ? psrt::psrt_reduce_lean : psrt::psrt_reduce,
+                         dim3(blocks, one ? (unsigned)nf : 1u), dim3(psrt::kReduceBlock), 0, st, ra);
       HIP_TRY(hipGetLastError());
     }
   }
@@ -1420,6 +1456,19 @@ static int get_default_context(rt_context** out, std::unique_lock<std::mutex>* l
   }
   *out = g_default[dev];
   (*out)->tune = tuning_defaults();  // the process defaults at each one-shot call
+  return RT_OK;
+}
+
+int rt_context_wait_drain(const rt_context* c, void* stream) {
+  if (!c) return set_error(RT_E_INVALID, "rt_context_wait_drain: ctx is NULL");
+  if (!c->d_drain)
+    return set_error(RT_E_HIP, "rt_context_wait_drain: no drain flag (signal memory unavailable)");
+  if (c->drain_epoch == 0) return RT_OK;  // nothing enqueued to wait for
+  HIP_TRY(hipSetDevice(c->device));
+  // the epoch of the context's last enqueued trace launch: set by its waves
+  // (a launch always empties its queue), and never lowered afterwards
+  HIP_TRY(hipStreamWaitValue64((hipStream_t)stream, c->d_drain, c->drain_epoch,
+                               hipStreamWaitValueGte));
   return RT_OK;
 }
 

@@ -115,6 +115,11 @@ struct TraceArgs {
   FastDiv div_s, div_w, div_p;      // unit / s_count, q / width, (f * pixels + q) / pixels
   unsigned flush_at;                // per-lane counters flush to the totals at this value
   int tail_prio;                    // raise the issue priority of waves whose queue is empty
+  // Drain flag (rt_context_wait_drain): every wave that finds the work queue
+  // empty stores drain_epoch here, so another stream can start the next
+  // frame's launch as this one's tail begins (nullptr: none)
+  unsigned long long* drain_flag;
+  unsigned long long drain_epoch;
 };
 
 // BVH node as the device reads it (two float4, from psrt_bvh.h BvhNode):
@@ -182,6 +187,7 @@ struct ReduceArgs {
   int s_count;
   int first_chunk;
   int spp_total;
+  double inv_spp;         // 1.0 / spp_total (psrt_reduce_lean: the division on the host)
   double* accum;          // [pixels][3] (required unless single chunk + rgb only)
   unsigned char* rgb8;    // [pixels][3] or nullptr (last chunk only)
   int fold_stats;         // block 0 folds the counter sets (one reduce per launch: frame 0's)
@@ -311,6 +317,11 @@ template <bool kBVH, bool kStamps, bool kLds, bool kCount>
 __global__ void psrt_trace(const double4* __restrict__ geo, const double* __restrict__ inv_r,
                            double* __restrict__ samples, TraceArgs a, BvhView bv);
 __global__ void psrt_reduce(ReduceArgs a);
+// psrt_reduce in 16 SGPRs, 32 VGPRs and no LDS: fits beside a resident
+// psrt_trace (Tuning reduce_lean; frames in flight); no statistics fold
+__global__ void psrt_reduce_lean(ReduceArgs a);
+// psrt_reduce's statistics fold alone, in psrt_reduce_lean's register budget
+__global__ void psrt_fold_stats(ReduceArgs a);
 __global__ void psrt_camera_lists(CamListArgs a);
 __global__ void psrt_quantize(const double* __restrict__ accum, unsigned char* __restrict__ rgb8,
                               unsigned n, int spp);

@@ -144,6 +144,8 @@ struct SectionClock {
   }
 };
 
+constexpr unsigned kDrainEvery = 64;  // workgroups per drain-flag writer (TraceArgs::drain_flag)
+
 struct RefillConst {
   // guided work queue phases (TraceArgs::ph_*), read when a wave takes a ticket
   uint64_t ph_first[kQueuePhases + 1];
@@ -155,6 +157,8 @@ struct RefillConst {
   uint64_t seedmix[kMaxFrames];  // splitmix64(seed of frame f) (TraceArgs::frames)
   FastDiv div_s, div_w, div_p;
   int hm1_i, row_offset, row_stride, s_begin, frames;
+  unsigned long long* drain_flag;  // TraceArgs::drain_flag / drain_epoch
+  unsigned long long drain_epoch;
 };
 
 __device__ __forceinline__ unsigned fast_div(unsigned n, const FastDiv& f) {
@@ -782,6 +786,11 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
     s_rc.row_offset = a.row_offset;
     s_rc.row_stride = a.row_stride;
     s_rc.s_begin = a.s_begin;
+    // one workgroup in kDrainEvery stores the drain flag: every store goes
+    // to the same host-visible word, and 12k of them (one per wave) queued
+    // behind each other cost ~1 ms per launch (profiles/r06_drain)
+    s_rc.drain_flag = blockIdx.x % kDrainEvery == 0 ? a.drain_flag : nullptr;
+    s_rc.drain_epoch = a.drain_epoch;
   }
   if constexpr (kLds) {  // the host sized the dynamic LDS by lds_layout
     for (int e = threadIdx.x; e < 2 * (bv.n_nodes + 1); e += blockDim.x) s_nodes[e] = bv.nodes[e];
@@ -985,6 +994,17 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void psrt_trace(const dou
           tailp = true;
           __builtin_amdgcn_s_setprio(kTailPrio);
         }
+        // the drain flag (read from LDS, a vector store): a launch waiting on
+        // another stream for this one's tail may start now
+#ifndef PSRT_NO_DRAIN_FLAG  // A/B builds only: without the store, rt_context_wait_drain never returns
+        if (lane == 0) {
+          unsigned zd = 0;
+          asm volatile("" : "+v"(zd));
+          const RefillConst& rd = *(const RefillConst*)((const char*)&s_rc + zd);
+          unsigned long long* const fl = rd.drain_flag;
+          if (fl) __hip_atomic_store(fl, rd.drain_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+#endif
         if constexpr (kStamps) {
           const unsigned long long t = __builtin_amdgcn_s_memrealtime();
           if (wlog && lane == 0) wlog[1] = t, wlog[3] = iters;
@@ -1194,7 +1214,9 @@ PSRT_INSTANTIATE(true, true, true)
 // pixel_color += sample, in sample order (main.cc:77-84); write_color on the
 // last chunk (color.h:8-24).
 
-__global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
+// Frame blockIdx.y's records and outputs; block 0 of frame 0 folds the trace
+// launch's counter sets and re-zeroes them and the queue heads.
+__device__ __forceinline__ void reduce_prologue(ReduceArgs& a) {
   if (blockIdx.y > 0) {  // frame blockIdx.y of a multi-frame launch
     const size_t f = blockIdx.y;
     a.samp_t += f * a.frame_units;
@@ -1218,6 +1240,24 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
     }
     if (threadIdx.x < kQueues) a.heads[kShardStride * threadIdx.x] = 0ull;
   }
+}
+
+// write_color (color.h:8-24) of one pixel's sums: 3 bytes in the low 24 bits
+__device__ __forceinline__ unsigned write_color_bytes(double r, double g, double b, double inv) {
+  const double c[3] = {r, g, b};
+  unsigned v = 0;
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    double x = __builtin_sqrt(c[ch] * inv);
+    x = (x < 0.0) ? 0.0 : x;  // std::max(x, 0.0)
+    x = (0.999 < x) ? 0.999 : x;  // std::min(x, 0.999)
+    v |= (unsigned)(unsigned char)(int)(255.999 * x) << (8 * ch);
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
+  reduce_prologue(a);
   // One wave per 64 pixels. A pixel's samples are contiguous, so the wave
   // stages [64 pixels][kReduceTile samples] tiles through LDS, then each lane
   // adds its pixel's samples in order.
@@ -1388,6 +1428,140 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
       }
     }
   }
+}
+
+// psrt_reduce beside a resident trace (frames in flight). A
+// psrt_trace launch holds 6 waves per SIMD at 80 VGPRs and ~150 KB of LDS per
+// CU, and its SGPRs (106, rounded up, plus the trap handler's 16) leave room
+// for one more wave per SIMD only if that wave needs at most 16 SGPRs, 32
+// VGPRs and no LDS (measured: scripts/coresident_probe.py, profiles/r06_drain).
+// psrt_reduce (252 VGPRs, 22 KB of LDS) waits for a free slot until the next
+// frame's trace drains; this variant starts at once beside it. To fit:
+//  - its arguments are read through a pointer held in a VGPR, so every value
+//    derived from them is per-lane; the few it branches or loops on are made
+//    scalar one at a time (readfirstlane);
+//  - no lane is masked off: a lane past the last pixel takes the last pixel
+//    and stores the same bytes there as its owner (identical values);
+//  - no statistics fold (the host launches psrt_reduce for a fold).
+// A lane per pixel reads its own records, four samples per step (32 B of t,
+// 8 B of k), and adds them in psrt_reduce's order with its operations:
+// bit-identical. fast_k and s_count % 4 == 0 only.
+template <class T>
+__device__ __forceinline__ T uniform(T v) {  // a wave-uniform value into one SGPR
+  return (T)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+__global__ __launch_bounds__(kReduceBlock) void psrt_reduce_lean(ReduceArgs) {
+  // beside a trace whose waves raise their priority to 1-3 in most sections,
+  // a priority-0 wave gets few issue slots: this one is short, so it goes first
+  __builtin_amdgcn_s_setprio(3);
+  uintptr_t ka = (uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+v"(ka));  // the argument block's address in a VGPR
+  const ReduceArgs* const ap = (const ReduceArgs*)ka;
+  const unsigned lane = threadIdx.x;
+  const unsigned f = blockIdx.y;
+  const unsigned pixels = ap->pixels;
+  const unsigned q0 = blockIdx.x * kReduceBlock;
+  const unsigned q = min(q0 + lane, pixels - 1);  // past the end: the last pixel again
+  const unsigned S = (unsigned)ap->s_count;
+  const unsigned width = ap->width;
+  // this lane's sums: element offsets (< 2^32: a launch's frames fit in memory)
+  const size_t apitch = ap->accum_pitch;
+  const unsigned aoff = (unsigned)(f * ap->accum_stride) +
+                        (apitch ? (q / width) * (unsigned)apitch + (q % width) * 3 : q * 3);
+  double* const acc_q = ap->accum + aoff;
+  double r = 0.0, g = 0.0, b = 0.0;
+  if (uniform(ap->first_chunk) == 0) {
+    r = acc_q[0];
+    g = acc_q[1];
+    b = acc_q[2];
+  }
+  const unsigned ro = f * (unsigned)ap->frame_units + q * S;
+  const double2* const tp = (const double2*)(ap->samp_t + ro);
+  const uint2* const kp = (const uint2*)(ap->samp_k + ro);
+  auto add = [&](double tt, unsigned kk) {
+    // psrt_reduce's operations, one channel at a time (fewer live registers)
+    const bool blk = kk == kSampleBlack;
+    const double w = 1.0 - tt;
+    r += blk ? 0.0 : __builtin_ldexp(w + tt * 0.5, -(int)kk);
+    __builtin_amdgcn_sched_barrier(0);
+    g += blk ? 0.0 : __builtin_ldexp(w + tt * 0.7, -(int)kk);
+    __builtin_amdgcn_sched_barrier(0);
+    b += blk ? 0.0 : __builtin_ldexp(w + tt * 1.0, -(int)kk);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  const unsigned steps = uniform(S / 4);
+#pragma unroll 1
+  for (unsigned st = 0; st < steps; ++st) {
+    const uint2 kk = kp[st];
+    const double2 t0 = tp[2 * st];
+    add(t0.x, kk.x & 0xffffu);
+    add(t0.y, kk.x >> 16);
+    const double2 t1 = tp[2 * st + 1];
+    add(t1.x, kk.y & 0xffffu);
+    add(t1.y, kk.y >> 16);
+  }
+  if (uniform(ap->accum != nullptr)) {
+    acc_q[0] = r;
+    acc_q[1] = g;
+    acc_q[2] = b;
+  }
+  if (uniform(ap->rgb8 != nullptr)) {  // write_color (color.h:8-24)
+    double inv = ap->inv_spp, hi = 0.999, sc = 255.999;
+    asm volatile("" : "+v"(hi), "+v"(sc));  // constants in VGPRs, not SGPR pairs
+    unsigned v = 0;
+    const double c[3] = {r, g, b};
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      double x = __builtin_sqrt(c[ch] * inv);
+      x = (x < 0.0) ? 0.0 : x;  // std::max(x, 0.0)
+      x = (hi < x) ? hi : x;    // std::min(x, 0.999)
+      v |= (unsigned)(unsigned char)(int)(sc * x) << (8 * ch);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const size_t rpitch = ap->rgb8_pitch;
+    unsigned char* const rgb = ap->rgb8 + f * ap->rgb8_stride;
+    unsigned char* const dst = rgb + (size_t)q0 * 3;
+    if (uniform(!rpitch && q0 + kReduceBlock <= pixels && ((uintptr_t)dst & 3u) == 0)) {
+      // the wave's 192 bytes as 48 dwords: dword l holds bytes 4l .. 4l + 3,
+      // from pixels 4l / 3 and the next (lane shuffles, no LDS allocation);
+      // lanes 48-63 store dword 47 again
+      const unsigned l = min(lane, (unsigned)kReduceBlock * 3 / 4 - 1);
+      const unsigned p0 = 4u * l / 3u;
+      const unsigned v0 = __shfl(v, p0), v1 = __shfl(v, min(p0 + 1, (unsigned)kReduceBlock - 1));
+      const uint64_t st = (uint64_t)v0 | ((uint64_t)v1 << 24);
+      ((unsigned*)dst)[l] = (unsigned)(st >> (8 * ((4u * l) % 3u)));
+    } else {
+      unsigned char* const px = rgb + (rpitch ? (q / width) * (unsigned)rpitch + (q % width) * 3
+                                              : q * 3);
+      px[0] = (unsigned char)v;
+      px[1] = (unsigned char)(v >> 8);
+      px[2] = (unsigned char)(v >> 16);
+    }
+  }
+}
+
+// reduce_prologue's statistics fold for psrt_reduce_lean's launches, in the
+// same register budget (arguments through a VGPR pointer): one wave.
+__global__ __launch_bounds__(64) void psrt_fold_stats(ReduceArgs) {
+  __builtin_amdgcn_s_setprio(3);
+  uintptr_t ka = (uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+v"(ka));
+  const ReduceArgs* const ap = (const ReduceArgs*)ka;
+  const unsigned t = threadIdx.x;
+  if (t < kStatWords) {
+    unsigned long long* const sets = ap->sets;
+    unsigned long long v = ap->first_chunk ? 0ull : ap->totals[t];
+#pragma unroll
+    for (int h = 0; h < kQueues; ++h) {
+      v += sets[kShardStride * h + t];
+      sets[kShardStride * h + t] = 0ull;
+    }
+    ap->totals[t] = v;
+    unsigned long long* const hs = ap->host_stats;
+    if (hs) hs[t] = v;
+  }
+  if (t < kQueues) ap->heads[kShardStride * t] = 0ull;
 }
 
 // ---- camera-ray candidate lists ------------------------------

@@ -409,6 +409,12 @@ class Context:
         check(self._L.rt_context_set_row_pitch(self.handle, accum_pitch, rgb8_pitch),
               "rt_context_set_row_pitch")
 
+    def wait_drain(self, stream: int) -> None:
+        """rt_context_wait_drain: `stream` waits until this context's last
+        enqueued trace launch has emptied its work queue, so a render enqueued
+        on it next (another context's frame) starts in this launch's tail."""
+        check(self._L.rt_context_wait_drain(self.handle, stream or None), "rt_context_wait_drain")
+
     def set_tuning(self, name: str, value: float) -> None:
         """rt_context_set_tuning on this context (measurement / test knobs)."""
         set_tuning(name, value, self)

@@ -38,7 +38,7 @@ def test_abi_version_and_info():
     L = _lib.load()
     hdr = open(os.path.join(ROOT, "include", "rt.h")).read()
     want = int(re.search(r"#define RT_ABI_VERSION (\d+)", hdr).group(1))
-    assert L.rt_abi_version() == want == _lib.ABI_VERSION == 6
+    assert L.rt_abi_version() == want == _lib.ABI_VERSION == 7
     assert b"gfx950" in L.rt_build_info()
 
 

@@ -18,7 +18,7 @@ TRACE_KNOBS = [
     ("queue_k", 1), ("queue_k", 5), ("queue_d", 1), ("queue_d", 8),
     ("no_fixpoint", 1), ("no_lds", 1), ("no_camlist", 1), ("no_neighbors", 1),
     ("blocks_per_cu", 1), ("blocks_per_cu", 2), ("big_ratio", 3), ("big_ratio", 1e4),
-    ("scene_rebuild", 1), ("flush_at", 1000),
+    ("scene_rebuild", 1), ("flush_at", 1000), ("reduce_lean", 1),
 ]
 MAT_KNOBS = [("mat_batch", 1), ("mat_batch", 64), ("mat_lds", 0), ("queue_k", 5),
              ("big_ratio", 3), ("no_camlist", 1)]
