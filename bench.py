@@ -471,10 +471,13 @@ def main():
         candidates = [(1, True)]
     else:
         candidates = [(1, True), (2, True), (3, True)]
-    depth = max(c[0] for c in candidates)  # contexts / buffers to allocate
+    depth = max(c[0] for c in candidates)
+    # contexts / buffers to allocate: the largest depth tried, and 2 for the
+    # one-frame-per-launch comparison beside a batched line (`unbatched`)
+    nslots = max(depth, 2 if B > 1 and not multi_chunk else 1)
     ctxs = []
     scene_ms = []  # rt_context_set_scene: host BVH / grid / neighbour lists + uploads
-    for _ in range(depth):
+    for _ in range(nslots):
         c = P.Context(local)
         t0 = time.perf_counter()
         c.set_scene(spheres, cam)
@@ -497,19 +500,19 @@ def main():
             raise SystemExit("--assemble host needs every rank on one node and no --gather-fp64")
     hostframes = None
     if assemble == "host":
-        hostframes = HostFrames(depth * B, h, w, rank, world)
+        hostframes = HostFrames(nslots * B, h, w, rank, world)
         for c in ctxs:
             c.set_row_pitch(0, world * w * 3)  # the sums stay packed on the device
     # per slot: B frames' accumulators and bytes
-    acc = [torch.zeros((B, rows, w, 3), dtype=torch.float64, device=dev) for _ in range(depth)]
+    acc = [torch.zeros((B, rows, w, 3), dtype=torch.float64, device=dev) for _ in range(nslots)]
     rgb = torch.zeros((h, w, 3), dtype=torch.uint8, device=dev) if rank == 0 and world > 1 else None  # --gather-fp64
     rgb_rows = [torch.zeros((B, rows, w, 3), dtype=torch.uint8, device=dev)
-                for _ in range(depth)] if assemble == "gather" else None
+                for _ in range(nslots)] if assemble == "gather" else None
     # every step ends with the frame's bytes in pinned host memory (rank 0):
     # per slot and frame, so frames in flight never share one
     host_rows = h if world > 1 else rows
     host_rgb = [torch.empty((B, host_rows, w, 3), dtype=torch.uint8, pin_memory=True)
-                for _ in range(depth)] if rank == 0 and assemble != "host" else None
+                for _ in range(nslots)] if rank == 0 and assemble != "host" else None
     # each frame slot renders on its context's own stream
     streams = [torch.cuda.ExternalStream(c.stream(), device=dev) for c in ctxs]
     # N > 1: every gather goes on one stream, in frame order on every rank
@@ -519,7 +522,7 @@ def main():
         if distributed:
             dist.barrier()
 
-    pending = [None] * depth  # per slot: (timed?, event after the gathers, frames)
+    pending = [None] * nslots  # per slot: (timed?, event after the gathers, frames)
     run = {"dn": depth, "kms": [], "rays": [], "exec": [], "frames": [], "prm": prm, "prev": None}
 
     def ptrs(t, nb):
@@ -603,7 +606,7 @@ def main():
                                 st["prerejects"], st["root_box_tests"]))
 
     def drain():
-        for k in range(depth):
+        for k in range(nslots):
             retire(k)
         torch.cuda.synchronize(dev)
 
@@ -667,7 +670,7 @@ def main():
     again = one(ctxs[0], 0)
     camlist_ms = max(0.0, (first["total_ms"] - first["kernel_ms"])
                      - (again["total_ms"] - again["kernel_ms"]))
-    for k in range(1, depth):
+    for k in range(1, nslots):
         one(ctxs[k], k)
     # A context's sample buffer grows to its largest render so far: one
     # untimed render of B frames per context here, so no timed launch
@@ -675,7 +678,7 @@ def main():
     # and the first timed launch would free and re-allocate B frames' records
     # inside the timed region: 0.5-0.8 ms, profiles/r04_timeline)
     if B > 1:
-        for k in range(depth):
+        for k in range(nslots):
             ctxs[k].render_device_frames(prm, B, ptrs(acc[k], B), None, streams[k].cuda_stream)
             ctxs[k].sync_stats()
     torch.cuda.synchronize(dev)
@@ -685,15 +688,15 @@ def main():
     tuning = {}
     if len(candidates) > 1:
         for c in candidates:
-            nt = max(6, 2 * c[0])
+            nt = max(10, 4 * c[0])
             tuning[str(c[0])] = timed(c[0], 1, nt, 1, c[1]) / nt * 1e3
-    # Frames in flight only for a clear gain (> 3% in the tuning runs): a
-    # pipelined run can settle into a schedule where two traces share the GPU
-    # and lose more
+    # Frames in flight for a gain over 1% in the tuning runs (each launch
+    # gated on the previous one's drain, each reduce beside the next trace:
+    # rt_context_wait_drain, psrt_reduce_lean)
     depth, tail_prio = candidates[0]
     if tuning:
         best = min(candidates, key=lambda c: tuning[str(c[0])])
-        if tuning[str(best[0])] < 0.97 * tuning[str(candidates[0][0])]:
+        if tuning[str(best[0])] < 0.99 * tuning[str(candidates[0][0])]:
             depth, tail_prio = best
     elapsed = timed(depth, args.warmup, args.steps, B, tail_prio)
     kernel_ms = sum(run["kms"]) / sum(run["frames"])  # device time of the trace per frame
@@ -711,11 +714,21 @@ def main():
     # when frames were in flight (their HIP events then span the other frames).
     unbatched = None
     if B > 1:
+        # one at a time, then two in flight (gated, the reduce beside the
+        # next trace): the faster is the one-frame-per-launch rate
         n1 = min(args.steps, 5)
         el1 = timed(1, 1, n1, 1)
-        unbatched = {"ms_per_step": round(el1 / n1 * 1e3, 3),
-                     "value": round((rows if args.emulate_shard else h) * w * spp * n1 / el1 / 1e6, 4),
-                     "kernel_ms": round(sum(run["kms"]) / sum(run["frames"]), 3)}
+        k1 = round(sum(run["kms"]) / sum(run["frames"]), 3)
+        n2 = min(args.steps, 10)
+        el2 = timed(2, 2, n2, 1) if nslots >= 2 else float("inf")
+        one_ms, two_ms = el1 / n1 * 1e3, el2 / n2 * 1e3
+        best_ms = min(one_ms, two_ms)
+        unbatched = {"ms_per_step": round(best_ms, 3),
+                     "value": round((rows if args.emulate_shard else h) * w * spp / best_ms / 1e3, 4),
+                     "frames_in_flight": 2 if two_ms < one_ms else 1,
+                     "ms_per_step_one_at_a_time": round(one_ms, 3),
+                     "ms_per_step_two_in_flight": round(two_ms, 3) if nslots >= 2 else None,
+                     "kernel_ms": k1}
     unpiped = None
     if depth > 1:
         n1 = min(args.steps, 3)
@@ -792,7 +805,7 @@ def main():
         # wrote into host memory against write_color of the gathered FP64 frame
         want = P.quantize(gathered.cpu().numpy(), spp)
         got = hostframes.frames[last_sl * B]
-        host_check = {"frames_in_host_memory": depth * B, "assembled_by": world,
+        host_check = {"frames_in_host_memory": nslots * B, "assembled_by": world,
                       "frame_equals_quantized_gathered_fp64": bool(np.array_equal(got, want))}
 
     if rank == 0:

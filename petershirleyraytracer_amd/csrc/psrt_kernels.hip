@@ -1446,15 +1446,21 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce(ReduceArgs a) {
 // A lane per pixel reads its own records, four samples per step (32 B of t,
 // 8 B of k), and adds them in psrt_reduce's order with its operations:
 // bit-identical. fast_k and s_count % 4 == 0 only.
+#ifndef PSRT_LEAN_PRIO
+#define PSRT_LEAN_PRIO 0  // issue priority of psrt_reduce_lean's waves (0 / 1 / 3: profiles/r06_drain)
+#endif
+
 template <class T>
 __device__ __forceinline__ T uniform(T v) {  // a wave-uniform value into one SGPR
   return (T)__builtin_amdgcn_readfirstlane((int)v);
 }
 
 __global__ __launch_bounds__(kReduceBlock) void psrt_reduce_lean(ReduceArgs) {
-  // beside a trace whose waves raise their priority to 1-3 in most sections,
-  // a priority-0 wave gets few issue slots: this one is short, so it goes first
-  __builtin_amdgcn_s_setprio(3);
+  // the trace beside it runs at priority 1-3 in most sections; a reduce wave
+  // at 0 still finishes within the trace (0.6 ms) and takes the fewest issue
+  // slots from it: C3 two in flight 11.83 ms per frame at 0, 11.87 at 1,
+  // 11.88 at 3 (profiles/r06_drain)
+  __builtin_amdgcn_s_setprio(PSRT_LEAN_PRIO);
   uintptr_t ka = (uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
   asm volatile("" : "+v"(ka));  // the argument block's address in a VGPR
   const ReduceArgs* const ap = (const ReduceArgs*)ka;
@@ -1544,7 +1550,7 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce_lean(ReduceArgs) {
 // reduce_prologue's statistics fold for psrt_reduce_lean's launches, in the
 // same register budget (arguments through a VGPR pointer): one wave.
 __global__ __launch_bounds__(64) void psrt_fold_stats(ReduceArgs) {
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(3);  // 5 us, and the reduce waits for it
   uintptr_t ka = (uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
   asm volatile("" : "+v"(ka));
   const ReduceArgs* const ap = (const ReduceArgs*)ka;

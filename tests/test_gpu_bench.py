@@ -65,6 +65,30 @@ def test_bench_single_gpu_line():
     assert rf["full_sphere_tests_per_launch"] > 0 and rf["frac"] > 0
 
 
+def test_bench_frames_in_flight_line():
+    """One frame per launch, two launches in flight (each gated on the
+    previous one's drain, each reduced by psrt_reduce_lean beside the next
+    trace): the timed frames are the reference's, and a batched line's
+    `unbatched` rate reports both schedules."""
+    _require_ref()
+    r = subprocess.run([sys.executable, "bench.py", "--config", "c2", "--steps", "6", "--warmup",
+                        "2", "--batch", "1", "--pipeline", "2", "--cpu-seconds", "1"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["frames_in_flight"] == 2 and d["frames_per_launch"] == 1
+    assert d["batch_check"]["last_frame_equal"] is True, d["batch_check"]
+    assert d["parity_vs_cpu"]["fp64_bit_identical"] is True
+    r = subprocess.run([sys.executable, "bench.py", "--config", "c2", "--steps", "4", "--warmup",
+                        "1", "--no-cpu-baseline"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=150)
+    assert r.returncode == 0, r.stderr[-3000:]
+    u = _last_json(r.stdout)["unbatched"]
+    assert u["frames_in_flight"] in (1, 2) and u["ms_per_step_one_at_a_time"] > 0
+    assert u["ms_per_step_two_in_flight"] > 0
+    assert u["ms_per_step"] == min(u["ms_per_step_one_at_a_time"], u["ms_per_step_two_in_flight"])
+
+
 def test_bench_two_ranks_gathered_frame_matches_reference():
     _require_ref()
     env = dict(os.environ, PSRT_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1",
