@@ -137,6 +137,10 @@ def parse():
     ap.add_argument("--no-drain-gate", action="store_true",
                     help="frames in flight: start the next launch at once instead of when the "
                          "previous one's work queue empties (rt_context_wait_drain; A/B)")
+    ap.add_argument("--chain", action="store_true",
+                    help="batched: also try the timed frames as a chain of B/2 or B/4-frame "
+                         "launches, two in flight, and keep the fastest (> 1%% gain; r06: C3 "
+                         "0.3-0.6%%, shards and C1 / C2 slower, so off by default)")
     ap.add_argument("--no-lean-reduce", action="store_true",
                     help="frames in flight: keep psrt_reduce instead of psrt_reduce_lean (A/B)")
     ap.add_argument("--scaling", default="strong", choices=("weak", "strong"),
@@ -465,6 +469,13 @@ def main():
     # Two persistent launches that share the GPU for their whole run are slower
     # than one after the other, so batches and multi-chunk frames run one at a
     # time; otherwise the depth is picked by measurement (`tuning` below).
+    # Batched: the timed frames in one launch, or (--chain) in launches of
+    # B / 2 or B / 4 frames, two in flight: each launch's tail filled by the
+    # next and its reduce beside the next trace, only the last exposed
+    # (picked by measurement like the one-frame depths; profiles/r06_drain)
+    chains = []
+    if B > 1 and not multi_chunk and args.chain and args.pipeline == 0:
+        chains = sorted({b2 for b2 in ((B + 1) // 2, (B + 3) // 4) if 1 < b2 < B}, reverse=True)
     if args.pipeline > 0:
         candidates = [(args.pipeline, True)]
     elif B > 1 or multi_chunk:
@@ -624,12 +635,11 @@ def main():
         dn launches in flight; the timed frames start from an idle GPU and end
         when the last one is done."""
         b = b or B
-        # frames in flight: each frame's reduce must fit beside the next
-        # frame's resident trace, or it waits for that trace's tail
-        # (psrt_reduce_lean, DESIGN.md §7); one launch at a time: psrt_reduce
+        # launches in flight: each launch's reduce must fit beside the next
+        # launch's resident trace, or it waits for that trace's tail
+        # (psrt_reduce_lean, DESIGN.md §7); the last launch's reduce, with no
+        # trace beside it, and one launch at a time: psrt_reduce (faster alone)
         lean = 1 if dn > 1 and not args.no_lean_reduce else 0
-        for c in ctxs:
-            c.set_tuning("reduce_lean", lean)
         run.update(dn=dn, kms=[], rays=[], exec=[], frames=[], prev=None,
                    prm=prm_count if count else (prm if tail else prm_notail))
         seq = [(nb, False) for nb in batches(nwarm, b)] + [(nb, True) for nb in batches(nsteps, b)]
@@ -642,6 +652,7 @@ def main():
                 t0 = time.perf_counter()
                 tl0 = time.monotonic_ns()
             retire(i % dn)  # the slot's previous launch must be done
+            ctxs[i % dn].set_tuning("reduce_lean", lean if i < len(seq) - 1 else 0)
             launch(i, nb, is_timed)
         if timeline:
             tl = time.monotonic_ns()
@@ -698,6 +709,14 @@ def main():
         best = min(candidates, key=lambda c: tuning[str(c[0])])
         if tuning[str(best[0])] < 0.99 * tuning[str(candidates[0][0])]:
             depth, tail_prio = best
+    if chains:
+        nt = args.steps
+        tuning[f"b{B}x1"] = timed(1, B, nt, B) / nt * 1e3
+        for b2 in chains:
+            tuning[f"b{b2}x2"] = timed(2, b2, nt, b2) / nt * 1e3
+        bb = min(chains, key=lambda b2: tuning[f"b{b2}x2"])
+        if tuning[f"b{bb}x2"] < 0.99 * tuning[f"b{B}x1"]:
+            B, depth = bb, 2
     elapsed = timed(depth, args.warmup, args.steps, B, tail_prio)
     kernel_ms = sum(run["kms"]) / sum(run["frames"])  # device time of the trace per frame
     rays = sum(run["rays"]) / sum(run["frames"])      # reference rays per frame
@@ -731,8 +750,10 @@ def main():
                      "kernel_ms": k1}
     unpiped = None
     if depth > 1:
-        n1 = min(args.steps, 3)
-        el1 = timed(1, 0, n1, 1)
+        # one launch (of the timed launches' size) at a time: the trace's
+        # device time per frame for the roofline, undisturbed by the overlap
+        n1 = B if B > 1 else min(args.steps, 3)
+        el1 = timed(1, 0, n1, B)
         kernel_ms = sum(run["kms"]) / sum(run["frames"])
         unpiped = {"ms_per_step": round(el1 / n1 * 1e3, 3),
                    "value": round((rows if args.emulate_shard else h) * w * spp * n1 / el1 / 1e6, 4)}

@@ -79,11 +79,17 @@ def test_bench_frames_in_flight_line():
     assert d["frames_in_flight"] == 2 and d["frames_per_launch"] == 1
     assert d["batch_check"]["last_frame_equal"] is True, d["batch_check"]
     assert d["parity_vs_cpu"]["fp64_bit_identical"] is True
-    r = subprocess.run([sys.executable, "bench.py", "--config", "c2", "--steps", "4", "--warmup",
-                        "1", "--no-cpu-baseline"], cwd=ROOT, capture_output=True, text=True,
+    r = subprocess.run([sys.executable, "bench.py", "--config", "c2", "--steps", "8", "--warmup",
+                        "2", "--no-cpu-baseline", "--chain"], cwd=ROOT, capture_output=True, text=True,
                        timeout=150)
     assert r.returncode == 0, r.stderr[-3000:]
-    u = _last_json(r.stdout)["unbatched"]
+    d = _last_json(r.stdout)
+    # batched: one launch of 8, or a chain of 4 / 2 in flight, whichever measured faster
+    tm = d["depth_tuning_ms"]
+    assert set(tm) == {"b8x1", "b4x2", "b2x2"}, tm
+    assert (d["frames_per_launch"], d["frames_in_flight"]) in ((8, 1), (4, 2), (2, 2))
+    assert d["batch_check"]["last_frame_equal"] is True, d["batch_check"]
+    u = d["unbatched"]
     assert u["frames_in_flight"] in (1, 2) and u["ms_per_step_one_at_a_time"] > 0
     assert u["ms_per_step_two_in_flight"] > 0
     assert u["ms_per_step"] == min(u["ms_per_step_one_at_a_time"], u["ms_per_step_two_in_flight"])
