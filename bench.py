@@ -485,7 +485,10 @@ def main():
     depth = max(c[0] for c in candidates)
     # contexts / buffers to allocate: the largest depth tried, and 2 for the
     # one-frame-per-launch comparison beside a batched line (`unbatched`)
-    nslots = max(depth, 2 if B > 1 and not multi_chunk else 1)
+    # (one process per GPU only: a rank's extra context is an extra stream
+    # and hardware queue, and 8 ranks sharing one GPU in the rehearsal then
+    # oversubscribe the queues: C3 8146 -> 7250-7470 Msamples/s, r06_final)
+    nslots = max(depth, 2 if B > 1 and not multi_chunk and world == 1 else 1)
     ctxs = []
     scene_ms = []  # rt_context_set_scene: host BVH / grid / neighbour lists + uploads
     for _ in range(nslots):
