@@ -513,8 +513,22 @@ def main():
         if assemble == "host" and (not one_node or args.gather_fp64):
             raise SystemExit("--assemble host needs every rank on one node and no --gather-fp64")
     hostframes = None
+    assemble_note = None
     if assemble == "host":
         hostframes = HostFrames(nslots * B, h, w, rank, world)
+        # every rank must have page-locked the shared frame; otherwise all of
+        # them fall back to the gather together (auto) or stop (--assemble host)
+        okt = torch.tensor([1 if hostframes.registered else 0], dtype=torch.int32,
+                           device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        if int(okt.item()) == 0:
+            why = hostframes.error or "another rank failed"
+            hostframes.close()
+            hostframes = None
+            if args.assemble == "host":
+                raise SystemExit(f"--assemble host: rt_host_register failed: {why}")
+            assemble, assemble_note = "gather", f"shared host frame unavailable ({why}): gather"
+    if assemble == "host":
         for c in ctxs:
             c.set_row_pitch(0, world * w * 3)  # the sums stay packed on the device
     # per slot: B frames' accumulators and bytes
@@ -927,7 +941,7 @@ def main():
                            + ("D2H: every rank's psrt_reduce writes its rows into one shared page-locked host frame" if assemble == "host" else
                               "D2H of the frame's bytes into pinned host memory (rank 0)" if world > 1 else
                               "D2H: psrt_reduce writes the frame's bytes into pinned host memory")),
-            "frame_to_host": assemble,
+            "frame_to_host": assemble if assemble_note is None else assemble_note,
             # one-time costs, outside the timed steps
             "one_time_ms": {"set_scene": round(scene_ms[0], 3),
                             "camera_lists": round(camlist_ms, 3),

@@ -130,8 +130,12 @@ class HostFrames:
                 self.shm.unlink()  # the mappings stay; nothing is left in /dev/shm
         self.frames = np.ndarray(self.shape, dtype=np.uint8, buffer=self.shm.buf)
         self.addr = C.addressof(C.c_ubyte.from_buffer(self.shm.buf))
-        _lib.check(self._L.rt_host_register(C.c_void_p(self.addr), size), "rt_host_register")
-        self.registered = True
+        # page-locking is per rank (and per device): a failure is reported in
+        # `registered` / `error` rather than raised, so the ranks can agree on
+        # a fallback together (bench.py) instead of one rank leaving the others
+        rc = self._L.rt_host_register(C.c_void_p(self.addr), size)
+        self.registered = rc == 0
+        self.error = None if self.registered else self._L.rt_last_error().decode(errors="replace")
         self.row_offset, self.row_stride = rank, world
 
     def rows_ptr(self, f: int, width: int) -> int:

@@ -83,3 +83,43 @@ def test_shard_math():
     for h in (1, 2, 7, 800, 2160):
         for world in (1, 2, 4, 8):
             assert sum(rows_owned(h, r, world) for r in range(world)) == h
+
+
+def _hostframes_worker(rank, world, port, out_path):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from petershirleyraytracer_amd.dist import HostFrames, rows_owned
+    nf, h, w = 2, 7, 5
+    hf = HostFrames(nf, h, w, rank, world)
+    # no device here: page-locking fails, reported (not raised) on every rank,
+    # so the ranks can fall back together (bench.py); the frame is still shared
+    assert hf.registered is False and hf.error
+    for f in range(nf):
+        for k in range(rows_owned(h, rank, world)):
+            row = rank + k * world
+            hf.frames[f, row] = 10 * f + row
+    dist.barrier()
+    if rank == 0:
+        np.save(out_path, np.array(hf.frames))
+    dist.barrier()
+    hf.close()
+    dist.destroy_process_group()
+
+
+def test_host_frames_shared_between_ranks(tmp_path):
+    """dist.HostFrames (the one-node frame-to-host route): the
+    ranks' interleaved rows land in one POSIX shared-memory frame that every
+    rank sees, and nothing is left in /dev/shm afterwards."""
+    world = 3
+    out = str(tmp_path / "hf.npy")
+    before = set(os.listdir("/dev/shm"))
+    mp.spawn(_hostframes_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    got = np.load(out)
+    want = np.zeros((2, 7, 5, 3), dtype=np.uint8)
+    for f in range(2):
+        for row in range(7):
+            want[f, row] = 10 * f + row
+    assert np.array_equal(got, want)
+    assert not [n for n in set(os.listdir("/dev/shm")) - before if n.startswith("psrt_")]
