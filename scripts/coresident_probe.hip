@@ -3,8 +3,8 @@
 // launch fills (6 waves per SIMD at 80 VGPRs, ~150 KB of LDS per CU)?
 // probe_stamp: one 64-thread workgroup per entry writes s_memrealtime
 // (100 MHz) at its start and spins `spin` ticks, so a caller sees when each
-// workgroup got a slot. Built by scripts/sessions/r06q.sh into
-// gpurun_out (hipcc -shared), loaded with ctypes.
+// workgroup got a slot. Built into gpurun_out by session Q (scripts/ARCHIVE.md,
+// hipcc -shared) and loaded with ctypes by scripts/coresident_probe.py.
 #include <hip/hip_runtime.h>
 
 __global__ __launch_bounds__(64) void probe_stamp(unsigned long long* out, unsigned spin) {
