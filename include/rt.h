@@ -184,7 +184,8 @@ int rt_context_set_row_pitch(rt_context* ctx, size_t accum_pitch, size_t rgb8_pi
  * flight). The wait holds however late it is enqueued: the
  * launch stores its number (counted per context, never reset) in a flag.
  * No-op before ctx's first render; RT_E_HIP if the device offers no signal
- * memory to wait on. */
+ * memory to wait on. ctx must outlive the wait: destroy it only after
+ * `stream` has passed it (e.g. after synchronising `stream`). */
 int rt_context_wait_drain(const rt_context* ctx, void* stream);
 
 /* Enqueue a render of the owned rows on `stream` (after the context's
