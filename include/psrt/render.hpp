@@ -55,11 +55,14 @@ struct basic_frame {
   std::vector<double, Alloc<double>> accum;        // rows x width x 3, reference order (top row first)
   std::vector<unsigned char, Alloc<unsigned char>> rgb8;  // write_color bytes
   rt_stats stats{};
+  // false: render_into (one device) fetches the bytes alone, what main.cc
+  // prints; the FP64 sums stay on the device (C3: 2.9 MB over the link, not 26)
+  bool want_accum = true;
   // sizes the buffers for a shard (no reallocation when they already fit)
   void shape(int w, int h, int samples, int row_offset, int row_stride) {
     width = w, height = h, spp = samples;
     rows = std::max(0, rt_rows_owned(h, row_offset, row_stride));  // a shard may own none
-    accum.resize((size_t)rows * w * 3);
+    accum.resize(want_accum ? (size_t)rows * w * 3 : 0);
     rgb8.resize((size_t)rows * w * 3);
   }
 };
@@ -127,8 +130,8 @@ inline void render_into(F& f, const hittable_list& world, const camera& cam, int
   p.row_offset = row_offset;
   p.row_stride = row_stride;
   f.shape(width, height, spp, row_offset, row_stride);
-  check(rt_render(spheres.data(), (int)spheres.size(), &c, &p, f.accum.data(), f.rgb8.data(),
-                  &f.stats),
+  check(rt_render(spheres.data(), (int)spheres.size(), &c, &p,
+                  f.want_accum ? f.accum.data() : nullptr, f.rgb8.data(), &f.stats),
         "rt_render");
 }
 
@@ -176,6 +179,7 @@ class device_group {
     p.row_offset = row_offset;
     p.row_stride = row_stride;
     p.flags = flags;
+    f.want_accum = true;  // a group gathers the sums too
     f.shape(width, height, spp, row_offset, row_stride);
     check(rt_group_render(g_, &p, f.accum.data(), f.rgb8.data(), &f.stats), "rt_group_render");
   }

@@ -239,7 +239,9 @@ int main(int argc, char** argv) {
     } else if (!devices.empty()) {
       f = psrt::render(world, cam, width, height, spp, depth, devices, seed, row_off, row_stride);
     } else {
-      f = psrt::render(world, cam, width, height, spp, depth, seed, row_off, row_stride);
+      // the bytes alone unless --accum asks for the sums (main.cc prints bytes)
+      f.want_accum = !accum_path.empty();
+      psrt::render_into(f, world, cam, width, height, spp, depth, seed, row_off, row_stride);
     }
     const double secs =
         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

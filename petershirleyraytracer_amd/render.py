@@ -242,12 +242,15 @@ def _out_arrays(out, rows: int, width: int, want_rgb: bool):
         return (np.zeros((rows, width, 3), dtype=np.float64),
                 np.zeros((rows, width, 3), dtype=np.uint8) if want_rgb else None)
     acc, rgb = out
-    if acc.shape != (rows, width, 3) or acc.dtype != np.float64 or not acc.flags.c_contiguous:
+    if acc is None and rgb is None:
+        raise ValueError("out needs at least one array")
+    if acc is not None and (acc.shape != (rows, width, 3) or acc.dtype != np.float64
+                            or not acc.flags.c_contiguous):
         raise ValueError(f"out accum must be C-contiguous float64 {(rows, width, 3)}")
     if rgb is not None and (rgb.shape != (rows, width, 3) or rgb.dtype != np.uint8
                             or not rgb.flags.c_contiguous):
         raise ValueError(f"out rgb8 must be C-contiguous uint8 {(rows, width, 3)}")
-    if not acc.flags.writeable or (rgb is not None and not rgb.flags.writeable):
+    if (acc is not None and not acc.flags.writeable) or (rgb is not None and not rgb.flags.writeable):
         raise ValueError("out arrays must be writeable")
     return acc, rgb
 
@@ -262,9 +265,11 @@ def render(spheres, camera, width: int, height: int, spp: int, max_depth: int = 
     cull_stats=True counts the executed sphere / box tests (tests_executed,
     box_tests; 0 otherwise) with the slower counting kernel, same bits.
     out=(accum, rgb8 or None): write into these arrays (e.g. host_array(...),
-    which the device writes directly) instead of new ones.
+    which the device writes directly) instead of new ones; out=(None, rgb8):
+    the write_color bytes only, what the reference's main() prints (the FP64
+    sums then stay on the device: 2.9 MB crosses the link for C3, not 26 MB).
 
-    Returns (accum[rows, W, 3] float64, rgb8[rows, W, 3] uint8 or None, stats dict).
+    Returns (accum[rows, W, 3] float64 or None, rgb8[rows, W, 3] uint8 or None, stats dict).
     """
     L = _lib.load()
     sp, n = _spheres(spheres)
@@ -278,7 +283,7 @@ def render(spheres, camera, width: int, height: int, spp: int, max_depth: int = 
     acc, rgb = _out_arrays(out, rows, width, want_rgb)
     st = RtStats()
     check(L.rt_render(sp, n, C.byref(cam), C.byref(p),
-                      acc.ctypes.data_as(C.POINTER(C.c_double)),
+                      acc.ctypes.data_as(C.POINTER(C.c_double)) if acc is not None else None,
                       rgb.ctypes.data_as(C.POINTER(C.c_ubyte)) if rgb is not None else None,
                       C.byref(st)), "rt_render")
     return acc, rgb, stats_dict(st)
@@ -474,6 +479,8 @@ class DeviceGroup:
         p = params(width, height, spp, max_depth, seed, row_offset, row_stride, flags)
         rows = max(0, self._L.rt_rows_owned(height, row_offset, row_stride))
         acc, rgb = _out_arrays(out, rows, width, want_rgb)
+        if acc is None:
+            raise ValueError("rt_group_render needs the accum array")
         st = RtStats()
         check(self._L.rt_group_render(self.handle, C.byref(p),
                                       acc.ctypes.data_as(C.POINTER(C.c_double)),

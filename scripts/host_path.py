@@ -20,9 +20,10 @@ ap.add_argument("--config", default="c3", choices=("c2", "c3", "c4"))
 ap.add_argument("--group", type=int, default=0,
                 help="render through rt_render_devices with this many members on device 0")
 ap.add_argument("--rows", default="", help="R/G: only rows R, R+G, ... (a C4 row band: 0/8)")
-ap.add_argument("--out", default="new", choices=("new", "reuse", "pinned"),
+ap.add_argument("--out", default="new", choices=("new", "reuse", "pinned", "pinned-bytes"),
                 help="outputs: new arrays per frame (pageable, first touch), the same pageable "
-                     "arrays every frame, or page-locked arrays (host_array) every frame")
+                     "arrays every frame, page-locked arrays (host_array) every frame, or the "
+                     "write_color bytes alone in a page-locked array (what main() prints)")
 args = ap.parse_args()
 w, h, spp = 1200, 800, 100
 if args.config == "c4":
@@ -38,6 +39,8 @@ if args.out == "reuse":
     out = (np.zeros(shape), np.zeros(shape, np.uint8))
 elif args.out == "pinned":
     out = (P.host_array(shape), P.host_array(shape, np.uint8))
+elif args.out == "pinned-bytes":
+    out = (None, P.host_array(shape, np.uint8))
 if args.group:
     grp = P.DeviceGroup([0] * args.group)
     grp.set_scene(sph, cam)
@@ -55,6 +58,6 @@ ms = 1e3 * sum(ts) / len(ts)
 print({"config": args.config, "rows": args.rows or "all", "group_members": args.group,
        "outputs": args.out,
        "frames": args.frames, "ms_per_frame_host_buffers": round(ms, 3),
-       "msamples_per_s_host_buffers": round(acc.shape[0] * w * spp / (ms * 1e-3) / 1e6, 1),
+       "msamples_per_s_host_buffers": round(shape[0] * w * spp / (ms * 1e-3) / 1e6, 1),
        "psrt_trace_ms": round(sum(ks) / len(ks), 3),
-       "host_bytes_per_frame": int(acc.nbytes + rgb.nbytes)})
+       "host_bytes_per_frame": int((acc.nbytes if acc is not None else 0) + rgb.nbytes)})

@@ -1,6 +1,7 @@
 // psrt::pinned_frame (page-locked host buffers, rt_host_alloc) against the
-// ordinary frame: the same bits through rt_render and rt_group_render, and a
-// pinned frame reused for a second render (tests/test_host_api.py).
+// ordinary frame: the same bits through rt_render and rt_group_render, a
+// pinned frame reused for a second render, and a bytes-only frame
+// (want_accum = false) (tests/test_host_api.py).
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -41,6 +42,11 @@ int main() {
   psrt::pinned_frame gf;
   g.render_into(gf, 96, 64, 8, 50, 5);
   if (!same(gf.accum, want.accum) || !same(gf.rgb8, want.rgb8)) return std::puts("group differs"), 1;
+  // the bytes alone (what main.cc prints): the sums stay on the device
+  psrt::pinned_frame bf;
+  bf.want_accum = false;
+  psrt::render_into(bf, world, cam, 96, 64, 8, 50, 5);
+  if (!bf.accum.empty() || !same(bf.rgb8, want.rgb8)) return std::puts("bytes-only differs"), 1;
   std::puts("ok");
   return 0;
 }

@@ -93,3 +93,16 @@ def test_row_pitch_shards_assemble_one_frame(final_scene, cam):
         ctxs[0].render_device(P.params(96, 64, 8, 50, 7, 0, 3), acc.data_ptr(), 0)
     for c in ctxs:
         c.close()
+
+
+def test_render_bytes_only(final_scene, cam):
+    """out=(None, rgb8): rt_render with no accum buffer (the reference main()'s
+    output): the sums stay on the device and the bytes equal a full render's,
+    into page-locked and pageable arrays alike."""
+    want, wrgb, ws = P.render(final_scene, cam, 96, 64, 8, seed=4)
+    for rgb in (P.host_array((64, 96, 3), np.uint8), np.zeros((64, 96, 3), np.uint8)):
+        acc, got, st = P.render(final_scene, cam, 96, 64, 8, seed=4, out=(None, rgb))
+        assert acc is None and got is rgb and np.array_equal(rgb, wrgb)
+        assert st["rays"] == ws["rays"]
+    with pytest.raises(ValueError):
+        P.render(final_scene, cam, 96, 64, 8, seed=4, out=(None, None))
