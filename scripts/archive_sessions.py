@@ -28,6 +28,16 @@ def main():
     if not paths:
         raise SystemExit(f"no scripts/sessions/{rnd}*.sh")
     rows = [f"| `{os.path.basename(p)}` | {header(p).replace('|', '/')} |" for p in paths]
+    archive = os.path.join(HERE, "ARCHIVE.md")
+    if f"## {rnd} sessions" in open(archive).read():
+        # a later batch of the same round: rows appended to its table (the
+        # round's section is the file's last), the commit named with them
+        with open(archive, "a") as f:
+            f.write("\n".join(r[:-1] + f" (commit `{commit}`) |" for r in rows) + "\n")
+        for p in paths:
+            os.remove(p)
+        print(f"archived {len(paths)} scripts")
+        return
     text = (f"\n## {rnd} sessions (removed at the end of {rnd})\n\n"
             f"The {rnd} `gpurun` command lists; each is in git history at commit "
             f"`{commit}` (`git show {commit}:scripts/sessions/<name>`). The records they "
