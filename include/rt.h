@@ -75,8 +75,9 @@ typedef struct {
 
 /* RNG streams. The reference draws from glibc rand() serially
  * (random.h:4-14), which no parallel device can reproduce; the device path
- * uses the COUNTER stream: one PCG32 stream per (pixel, sample), fed through
- * the reference's own random_double() mapping. See DESIGN.md §RNG. */
+ * uses the COUNTER stream: one xorshift32 + Weyl stream per (pixel, sample)
+ * (PCG32 until r05), fed through the reference's own random_double() mapping.
+ * See DESIGN.md §RNG. */
 #define RT_RNG_COUNTER 0
 
 /* flags */

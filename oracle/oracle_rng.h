@@ -10,13 +10,16 @@
  *    dependency: glibc 2.35 (this image's libc); tests pin this restatement
  *    against the real rand().
  *
- * 2. COUNTER: the device contract. One PCG32 (XSH-RR, O'Neill 2014) stream per
- *    (pixel, sample):  key   = (uint64)(j*W + i) << 32 | s   (reference j:
+ * 2. COUNTER: the device contract. One stream per (pixel, sample):
+ *                      key   = (uint64)(j*W + i) << 32 | s   (reference j:
  *                              0 = bottom row, main.cc:72; s = sample index)
  *                      state = splitmix64(key ^ splitmix64(seed))
- *    Each rand() returns pcg32() >> 1 (31 bits, the range of glibc rand()),
- *    so the reference's random_double() = rand()/(RAND_MAX+1.0) maps it to
- *    [0,1) unchanged.
+ *    state = {w: high 32 bits, x: low 32 bits}; each draw steps
+ *    x = xorshift32(x) (Marsaglia's 13, 17, 5), w += 0x9E3779B9, and rand()
+ *    returns (x + w) >> 1 (31 bits, the range of glibc rand()), so the
+ *    reference's random_double() = rand()/(RAND_MAX+1.0) maps it to [0,1)
+ *    unchanged. (r01-r05: PCG32 XSH-RR; replaced in r06 by this 32-bit-op
+ *    generator)
  *
  * random_double() here is the reference's INTENDED mapping
  * (double)rand() / (RAND_MAX + 1.0); the shipped random.h:7 computes
@@ -79,17 +82,19 @@ static inline uint64_t oracle_stream_state(uint64_t seed, uint32_t pixel,
   return oracle_splitmix64(key ^ oracle_splitmix64(seed));
 }
 
-static inline uint32_t oracle_pcg32(uint64_t* state) {
-  uint64_t old = *state;
-  uint32_t xs, rot;
-  *state = old * 6364136223846793005ULL + 1442695040888963407ULL;
-  xs = (uint32_t)(((old >> 18) ^ old) >> 27);
-  rot = (uint32_t)(old >> 59);
-  return (xs >> rot) | (xs << ((32u - rot) & 31u));
+/* one draw's raw 32 bits (rand() = raw >> 1); device: psrt_device.h rand31 */
+static inline uint32_t oracle_counter_raw(uint64_t* state) {
+  uint32_t x = (uint32_t)*state;
+  uint32_t w = (uint32_t)(*state >> 32) + 0x9E3779B9u;
+  x ^= x << 13;
+  x ^= x >> 17;
+  x ^= x << 5;
+  *state = ((uint64_t)w << 32) | x;
+  return x + w;
 }
 
 static inline int32_t oracle_counter_rand(uint64_t* state) {
-  return (int32_t)(oracle_pcg32(state) >> 1);
+  return (int32_t)(oracle_counter_raw(state) >> 1);
 }
 
 #endif /* PSRT_ORACLE_RNG_H */

@@ -18,13 +18,30 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   return z ^ (z >> 31);
 }
 
-// PCG32 XSH-RR step; returns the 31-bit value the reference's rand() yields.
+// The counter stream's generator: a sample's 64-bit
+// state is {w: high word, x: low word}; each draw steps x by Marsaglia's
+// xorshift32 (13, 17, 5), adds 0x9E3779B9 to w (a Weyl sequence, period 2^32
+// per sample: distinct samples' xorshift runs that overlap still differ by
+// their w), and returns raw = x + w; rand() = raw >> 1 (31 bits, the range of
+// glibc rand()). 32-bit operations only: r05's PCG32 needed a 64-bit multiply
+// per draw, and the look-ahead trials cost 3.5% more kernel time with it
+// (profiles/r06_rngcost). A zero x stays zero (the draws are then the Weyl
+// sequence alone), identically in the oracle and the reference's interposer.
+constexpr uint32_t kWeyl = 0x9E3779B9u;
+
+__device__ __forceinline__ uint32_t xorshift32(uint32_t x) {
+  x ^= x << 13;
+  x ^= x >> 17;
+  x ^= x << 5;
+  return x;
+}
+
+// One draw; returns rand().
 __device__ __forceinline__ uint32_t rand31(uint64_t& st) {
-  const uint64_t old = st;
-  st = old * 6364136223846793005ULL + 1442695040888963407ULL;
-  const uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
-  const uint32_t rot = (uint32_t)(old >> 59);
-  return ((xs >> rot) | (xs << ((32u - rot) & 31u))) >> 1;
+  const uint32_t x = xorshift32((uint32_t)st);
+  const uint32_t w = (uint32_t)(st >> 32) + kWeyl;
+  st = ((uint64_t)w << 32) | x;
+  return (x + w) >> 1;
 }
 
 // random_double(): (double)rand() / (RAND_MAX + 1.0). The divisor is 2^31, so
@@ -33,26 +50,19 @@ __device__ __forceinline__ double random_double(uint64_t& st) {
   return (double)rand31(st) * 0x1p-31;
 }
 
-// The raw PCG32 XSH-RR output of state `old` (32 bits); rand() = raw >> 1.
-__device__ __forceinline__ uint32_t pcg_raw32(uint64_t old) {
-  const uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
-  const uint32_t rot = (uint32_t)(old >> 59);
-  return (xs >> rot) | (xs << ((32u - rot) & 31u));
-}
-
-// Three consecutive raw draws with the LCG jumped ahead: s1 = a s0 + c,
-// s2 = a^2 s0 + c (a + 1), s3 = a^3 s0 + c (a^2 + a + 1) (mod 2^64) — the
-// states of three consecutive PCG32 steps, from independent multiplies.
-// rand() = raw >> 1 (see pm1_raw); `next` is the state after the third draw.
+// Three consecutive raw draws (rand() = raw >> 1, see pm1_raw): the Weyl
+// words of the three steps are independent adds; `next` is the state after
+// the third draw.
 __device__ __forceinline__ void raw32_x3(uint64_t s0, uint32_t& r0, uint32_t& r1, uint32_t& r2,
                                          uint64_t& next) {
-  const uint64_t s1 = s0 * 6364136223846793005ULL + 1442695040888963407ULL;
-  const uint64_t s2 = s0 * 0x685f98a2018fade9ULL + 0x1a08ee1184ba6d32ULL;
-  const uint64_t s3 = s0 * 0x0b046976f22528f5ULL + 0x9af678222e728119ULL;
-  r0 = pcg_raw32(s0);
-  r1 = pcg_raw32(s1);
-  r2 = pcg_raw32(s2);
-  next = s3;
+  const uint32_t w = (uint32_t)(s0 >> 32);
+  const uint32_t x1 = xorshift32((uint32_t)s0);
+  const uint32_t x2 = xorshift32(x1);
+  const uint32_t x3 = xorshift32(x2);
+  r0 = x1 + (w + kWeyl);
+  r1 = x2 + (w + 2u * kWeyl);
+  r2 = x3 + (w + 3u * kWeyl);
+  next = ((uint64_t)(w + 3u * kWeyl) << 32) | x3;
 }
 
 // random_double(-1, 1) = -1 + 2 * (rand() * 2^-31) (random.h:10-14) of the draw
