@@ -9,7 +9,7 @@
 //  * rand() interposition: the reference calls glibc rand() through
 //    random_double() (random.h:4-14). In --rng glibc mode rand() is glibc's
 //    own generator (random(), which glibc's rand() wraps); in --rng counter
-//    mode it returns the per-(pixel, sample) PCG32 stream of
+//    mode it returns the per-(pixel, sample) counter stream (xorshift32 + Weyl) of
 //    oracle/oracle_rng.h, reseeded before each sample — the device contract.
 //  * A copy of the main.cc:72-88 pixel loop with W/H/spp/depth/shard
 //    parameters, calling the reference ray_color() and write_color().
