@@ -1467,6 +1467,7 @@ __global__ __launch_bounds__(kReduceBlock) void psrt_reduce_lean(ReduceArgs) {
   const unsigned lane = threadIdx.x;
   const unsigned f = blockIdx.y;
   const unsigned pixels = ap->pixels;
+  if (uniform(pixels) == 0) return;  // (the host launches no empty reduce; kept exact anyway)
   const unsigned q0 = blockIdx.x * kReduceBlock;
   const unsigned q = min(q0 + lane, pixels - 1);  // past the end: the last pixel again
   const unsigned S = (unsigned)ap->s_count;
