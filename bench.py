@@ -137,6 +137,9 @@ def parse():
     ap.add_argument("--no-drain-gate", action="store_true",
                     help="frames in flight: start the next launch at once instead of when the "
                          "previous one's work queue empties (rt_context_wait_drain; A/B)")
+    ap.add_argument("--no-tail-priority", action="store_true",
+                    help="with --pipeline: the draining waves keep their base issue priority "
+                         "(RT_FLAG_NO_TAIL_PRIORITY; A/B)")
     ap.add_argument("--chain", action="store_true",
                     help="batched: also try the timed frames as a chain of B/2 or B/4-frame "
                          "launches, two in flight, and keep the fastest (> 1%% gain; r06: C3 "
@@ -477,7 +480,7 @@ def main():
     if B > 1 and not multi_chunk and args.chain and args.pipeline == 0:
         chains = sorted({b2 for b2 in ((B + 1) // 2, (B + 3) // 4) if 1 < b2 < B}, reverse=True)
     if args.pipeline > 0:
-        candidates = [(args.pipeline, True)]
+        candidates = [(args.pipeline, not args.no_tail_priority)]
     elif B > 1 or multi_chunk:
         candidates = [(1, True)]
     else:
